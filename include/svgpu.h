@@ -1,0 +1,125 @@
+/*
+ * svgpu.h -- C ABI of the MI355X-native BN254 MSM + KZG-decider backend (libsvgpu.so).
+ *
+ * Drop-in boundary for snark-verifier's native hot path (yuliakot/snark-verifier-axiom):
+ *
+ *   sv_bn254_g1_msm          replaces  NativeLoader::multi_scalar_multiplication
+ *                                      snark-verifier/src/loader/native.rs:61-71
+ *                            and       util::msm::multi_scalar_multiplication
+ *                                      snark-verifier/src/util/msm.rs:287-316
+ *   sv_bn254_kzg_decide      replaces  AccumulationDecider::{decide, decide_all} for KzgAs on NativeLoader
+ *                                      snark-verifier/src/pcs/kzg/decider.rs:60-68 and :70-80
+ *   sv_bn254_kzg_accumulate  replaces  KzgAs::create_proof's two MSMs (no zk blind)
+ *                                      snark-verifier/src/pcs/kzg/accumulation.rs:146-195
+ *                                      (also AccumulationScheme::verify, :40-62)
+ *
+ * The Rust binding a maintainer adds is in INTEGRATION.md.  Conventions:
+ *  - every function is extern "C", never throws, and returns an sv_status;
+ *  - every pointer is caller-owned and borrowed for the call only; nothing is retained;
+ *  - field elements are 4 x u64 little-endian limbs (= halo2curves' in-memory Fq/Fr layout);
+ *    `form` says whether inputs/outputs are canonical (SV_CANONICAL) or Montgomery with
+ *    R = 2^256 (SV_MONTGOMERY, zero-copy with halo2curves memory);
+ *  - the affine identity is (0, 0), as halo2curves encodes it;
+ *  - calls are re-entrant: each call draws a stream + workspace from a per-device pool.
+ *  - there is NO CPU fallback inside this library: without a usable GPU every compute entry
+ *    point returns SV_ERR_DEVICE (the Rust shim then keeps the reference's own CPU code path).
+ */
+#ifndef SVGPU_H_
+#define SVGPU_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+#define SV_NOEXCEPT noexcept
+extern "C" {
+#else
+#define SV_NOEXCEPT
+#endif
+
+#define SVGPU_ABI_VERSION 1
+
+typedef struct { uint64_t l[4]; } sv_fe;                 /* Fq or Fr element                     */
+typedef struct { sv_fe x, y; } sv_g1_affine;             /* identity = all-zero                  */
+typedef struct { sv_fe x, y, z; } sv_g1_jacobian;        /* x = X/Z^2, y = Y/Z^3; identity Z = 0 */
+typedef struct { sv_fe c0, c1; } sv_fq2;                 /* c0 + c1*u, u^2 = -1                  */
+typedef struct { sv_fq2 x, y; } sv_g2_affine;            /* D-type twist coords; identity = 0    */
+typedef struct { sv_fq2 c[6]; } sv_fq12;                 /* c0.c0 c0.c1 c0.c2 c1.c0 c1.c1 c1.c2  */
+
+enum sv_form { SV_CANONICAL = 0, SV_MONTGOMERY = 1 };
+
+enum sv_status {
+  SV_OK = 0,
+  SV_ERR_EMPTY = 1,  /* n == 0: "pairs should not be empty" (native.rs:69) / decider.rs:74 */
+  SV_ERR_LEN = 2,    /* size too large for the device workspace                            */
+  SV_ERR_ARG = 3,    /* null pointer, bad form, non-reduced element, point not on curve    */
+  SV_ERR_DEVICE = 4, /* no usable GPU, or a HIP runtime error                              */
+  SV_ERR_OOM = 5     /* device allocation failed                                           */
+};
+
+/* ---- runtime ---------------------------------------------------------------------- */
+int sv_init(int num_devices) SV_NOEXCEPT;        /* idempotent; <= 0 means every visible device      */
+int sv_device_count(void) SV_NOEXCEPT;           /* devices initialised (0 before sv_init / no GPU)  */
+const char* sv_last_error(void) SV_NOEXCEPT;     /* thread-local message for the last non-OK status  */
+const char* sv_version(void) SV_NOEXCEPT;
+
+/* ---- a1/a3: multi-scalar multiplication ---------------------------------------------
+ * out = sum_i scalars[i] * bases[i] as an affine point (identity -> (0,0)).
+ * Host buffers.  num_gpus <= 0 means every initialised device (point-sharded, partials
+ * folded in device order).  Scalars must be reduced (< r) in the given form.              */
+int sv_bn254_g1_msm(const sv_g1_affine* bases, const sv_fe* scalars, size_t n, int form,
+                    int num_gpus, sv_g1_affine* out) SV_NOEXCEPT;
+
+/* Device-resident variant (bases/scalars already in HBM on `device`, `stream` may be NULL):
+ * writes this shard's partial sum to *out_partial (host memory, Jacobian, canonical form).
+ * This is the per-rank step of the RCCL-sharded MSM (one process per GPU).              */
+int sv_bn254_g1_msm_device(const sv_g1_affine* d_bases, const sv_fe* d_scalars, size_t n,
+                           int form, int device, void* stream, sv_g1_jacobian* out_partial) SV_NOEXCEPT;
+
+/* Fold Jacobian partials (canonical form) in index order and convert to affine.  Host-only
+ * (no GPU needed): the combine step after the RCCL all-gather of per-rank partials.      */
+int sv_bn254_g1_fold(const sv_g1_jacobian* partials, size_t k, sv_g1_affine* out, int out_form) SV_NOEXCEPT;
+
+/* ---- a7/a8: KZG decider ----------------------------------------------------------------
+ * For every i: e(lhs[i], g2) * e(rhs[i], -s_g2) == 1 ?  *first_fail = first failing index, or
+ * -1 when all pass (the reference returns Err(AssertionFailure) on the first failure).
+ * Identity G1 inputs contribute 1, as halo2curves' multi_miller_loop skips them.          */
+int sv_bn254_kzg_decide(const sv_g2_affine* g2, const sv_g2_affine* s_g2,
+                        const sv_g1_affine* lhs, const sv_g1_affine* rhs, size_t n, int form,
+                        int num_gpus, int32_t* first_fail) SV_NOEXCEPT;
+
+/* Device-resident variant; optional per-accumulator outputs:
+ *   verdicts (host, n int32: 1 = pass) and gt (host, n sv_fq12, canonical: the value
+ *   e(lhs,g2)*e(rhs,-s_g2) after final exponentiation, for Gt-value parity tests).        */
+int sv_bn254_kzg_decide_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2,
+                               const sv_g1_affine* d_lhs, const sv_g1_affine* d_rhs, size_t n,
+                               int form, int device, void* stream, int32_t* first_fail,
+                               int32_t* verdicts, sv_fq12* gt) SV_NOEXCEPT;
+
+/* ---- a10: KZG accumulation (KzgAs::create_proof / verify without blind) -----------------
+ * out_lhs = sum_i r^i lhs[i], out_rhs = sum_i r^i rhs[i], r^0 = 1 (loader.rs:71-78).       */
+int sv_bn254_kzg_accumulate(const sv_g1_affine* lhs, const sv_g1_affine* rhs, size_t n,
+                            const sv_fe* r, int form, int num_gpus, sv_g1_affine* out_lhs,
+                            sv_g1_affine* out_rhs) SV_NOEXCEPT;
+
+/* ---- synthetic inputs (SURVEY.md section 8d generator, index-addressable) -------------
+ * Fills device buffers with the deterministic SplitMix64 scalars / try-and-increment bases
+ * (elements start .. start+n-1) in the requested form.                                   */
+int sv_gen_scalars_device(sv_fe* d_scalars, size_t n, uint64_t seed, uint64_t start, int form,
+                          int device, void* stream) SV_NOEXCEPT;
+int sv_gen_bases_device(sv_g1_affine* d_bases, size_t n, uint64_t seed, uint64_t start, int form,
+                        int device, void* stream) SV_NOEXCEPT;
+
+/* ---- instrumentation ----------------------------------------------------------------
+ * Per-kernel timings (HIP events on the call's stream) of the last MSM on this thread.   */
+typedef struct {
+  float total_ms, digits_ms, sort_ms, accumulate_ms, fixup_ms, reduce_ms, host_ms;
+  uint32_t window_bits, num_windows, accumulate_launch_units;
+  uint64_t entries;
+} sv_msm_stats;
+int sv_msm_last_stats(sv_msm_stats* out) SV_NOEXCEPT;
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SVGPU_H_ */

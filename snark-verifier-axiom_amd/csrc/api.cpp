@@ -1,0 +1,339 @@
+// C ABI of libsvgpu (include/svgpu.h).  Every entry point is noexcept and maps failures to
+// sv_status codes with a thread-local message (sv_last_error).  No CPU fallback: compute entry
+// points need a GPU and return SV_ERR_DEVICE without one.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <exception>
+#include <thread>
+#include <vector>
+
+#include "../../include/svgpu.h"
+#include "decider.hpp"
+#include "gen.hpp"
+#include "host_ec.hpp"
+#include "msm.hpp"
+#include "runtime.hpp"
+
+using namespace sv;
+using sv::host::F;
+using sv::host::Xyzz;
+
+namespace {
+
+F fe_in(const sv_fe& a) {
+  F r;
+  memcpy(r.l, a.l, 32);
+  return r;
+}
+sv_fe fe_out(const F& a) {
+  sv_fe r;
+  memcpy(r.l, a.l, 32);
+  return r;
+}
+
+void affine_out(const Xyzz& p, int form, sv_g1_affine* out) {
+  F x, y;
+  host::x_to_affine(p, x, y);
+  if (form == SV_CANONICAL && !host::x_is_identity(p)) {
+    x = host::f_from_mont(x);
+    y = host::f_from_mont(y);
+  }
+  out->x = fe_out(x);
+  out->y = fe_out(y);
+}
+
+void jacobian_out(const Xyzz& p, sv_g1_jacobian* out) {
+  F X, Y, Z;
+  host::x_to_jacobian(p, X, Y, Z);
+  out->x = fe_out(host::f_from_mont(X));
+  out->y = fe_out(host::f_from_mont(Y));
+  out->z = fe_out(host::f_from_mont(Z));
+}
+
+int resolve_gpus(int num_gpus) {
+  int have = runtime_device_count();
+  if (have == 0) {
+    if (runtime_init(0) != SV_OK) return 0;
+    have = runtime_device_count();
+  }
+  if (num_gpus <= 0 || num_gpus > have) return have;
+  return num_gpus;
+}
+
+// Runs fn(shard_index, device) on one host thread per device; returns the first non-OK status.
+template <class Fn>
+int for_each_device(int ndev, Fn fn) {
+  std::vector<int> rc(ndev, SV_OK);
+  std::vector<std::string> msg(ndev);
+  if (ndev == 1) return fn(0, runtime_device_id(0));
+  std::vector<std::thread> th;
+  for (int d = 0; d < ndev; d++)
+    th.emplace_back([&, d] {
+      rc[d] = fn(d, runtime_device_id(d));
+      if (rc[d] != SV_OK) msg[d] = sv::last_error();
+    });
+  for (auto& t : th) t.join();
+  for (int d = 0; d < ndev; d++)
+    if (rc[d] != SV_OK) {
+      sv::set_error("device %d: %s", d, msg[d].c_str());
+      return rc[d];
+    }
+  return SV_OK;
+}
+
+// Owned device buffer on `device` (host-buffer API path).
+struct DevBuf {
+  void* p = nullptr;
+  int dev = 0;
+  ~DevBuf() {
+    if (p) {
+      hipSetDevice(dev);
+      hipFree(p);
+    }
+  }
+  int alloc(int device, size_t bytes) {
+    dev = device;
+    SV_HIP(hipSetDevice(device));
+    SV_HIP(hipMalloc(&p, bytes ? bytes : 1));
+    return SV_OK;
+  }
+};
+
+#define SV_GUARD_BEGIN try {
+#define SV_GUARD_END                                    \
+  }                                                     \
+  catch (const std::exception& e) {                     \
+    sv::set_error("internal error: %s", e.what());      \
+    return SV_ERR_DEVICE;                               \
+  }                                                     \
+  catch (...) {                                         \
+    sv::set_error("internal error");                    \
+    return SV_ERR_DEVICE;                               \
+  }
+
+int check_form(int form) {
+  if (form != SV_CANONICAL && form != SV_MONTGOMERY) {
+    sv::set_error("bad form %d", form);
+    return SV_ERR_ARG;
+  }
+  return SV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sv_init(int num_devices) noexcept {
+  SV_GUARD_BEGIN
+  return runtime_init(num_devices);
+  SV_GUARD_END
+}
+
+int sv_device_count(void) noexcept {
+  SV_GUARD_BEGIN
+  return runtime_device_count();
+  SV_GUARD_END
+}
+
+const char* sv_last_error(void) noexcept { return sv::last_error(); }
+
+const char* sv_version(void) noexcept { return "svgpu 0.1.0 (abi 1, gfx950)"; }
+
+int sv_bn254_g1_msm(const sv_g1_affine* bases, const sv_fe* scalars, size_t n, int form, int num_gpus,
+                    sv_g1_affine* out) noexcept {
+  SV_GUARD_BEGIN
+  if (n == 0) {
+    sv::set_error("pairs should not be empty");
+    return SV_ERR_EMPTY;
+  }
+  if (!bases || !scalars || !out) {
+    sv::set_error("null pointer");
+    return SV_ERR_ARG;
+  }
+  SV_TRY(check_form(form));
+  int ndev = resolve_gpus(num_gpus);
+  if (ndev == 0) return SV_ERR_DEVICE;
+  if ((size_t)ndev > n) ndev = (int)n;
+  std::vector<Xyzz> part(ndev, host::x_identity());
+  size_t per = (n + ndev - 1) / ndev;
+  int rc = for_each_device(ndev, [&](int k, int dev) -> int {
+    size_t lo = k * per, hi = std::min(n, lo + per);
+    if (lo >= hi) return SV_OK;
+    size_t m = hi - lo;
+    DevBuf db, ds;
+    SV_TRY(db.alloc(dev, m * sizeof(sv_g1_affine)));
+    SV_TRY(ds.alloc(dev, m * sizeof(sv_fe)));
+    SV_HIP(hipMemcpy(db.p, bases + lo, m * sizeof(sv_g1_affine), hipMemcpyHostToDevice));
+    SV_HIP(hipMemcpy(ds.p, scalars + lo, m * sizeof(sv_fe), hipMemcpyHostToDevice));
+    return msm_run_device(db.p, ds.p, m, form, dev, nullptr, &part[k]);
+  });
+  if (rc != SV_OK) return rc;
+  Xyzz acc = host::x_identity();
+  for (auto& p : part) acc = host::x_add(acc, p);
+  affine_out(acc, form, out);
+  return SV_OK;
+  SV_GUARD_END
+}
+
+int sv_bn254_g1_msm_device(const sv_g1_affine* d_bases, const sv_fe* d_scalars, size_t n, int form,
+                           int device, void* stream, sv_g1_jacobian* out_partial) noexcept {
+  SV_GUARD_BEGIN
+  if (n == 0) {
+    sv::set_error("pairs should not be empty");
+    return SV_ERR_EMPTY;
+  }
+  if (!d_bases || !d_scalars || !out_partial) {
+    sv::set_error("null pointer");
+    return SV_ERR_ARG;
+  }
+  SV_TRY(check_form(form));
+  if (resolve_gpus(0) == 0) return SV_ERR_DEVICE;
+  Xyzz r;
+  SV_TRY(msm_run_device(d_bases, d_scalars, n, form, device, (hipStream_t)stream, &r));
+  jacobian_out(r, out_partial);
+  return SV_OK;
+  SV_GUARD_END
+}
+
+int sv_bn254_g1_fold(const sv_g1_jacobian* partials, size_t k, sv_g1_affine* out, int out_form) noexcept {
+  SV_GUARD_BEGIN
+  if (k == 0) {
+    sv::set_error("no partials");
+    return SV_ERR_EMPTY;
+  }
+  if (!partials || !out) {
+    sv::set_error("null pointer");
+    return SV_ERR_ARG;
+  }
+  SV_TRY(check_form(out_form));
+  Xyzz acc = host::x_identity();
+  for (size_t i = 0; i < k; i++) {
+    F X = fe_in(partials[i].x), Y = fe_in(partials[i].y), Z = fe_in(partials[i].z);
+    if (!host::f_is_reduced(X) || !host::f_is_reduced(Y) || !host::f_is_reduced(Z)) {
+      sv::set_error("partial %zu: coordinate not reduced", i);
+      return SV_ERR_ARG;
+    }
+    acc = host::x_add(acc, host::x_from_jacobian(host::f_to_mont(X), host::f_to_mont(Y), host::f_to_mont(Z)));
+  }
+  affine_out(acc, out_form, out);
+  return SV_OK;
+  SV_GUARD_END
+}
+
+int sv_bn254_kzg_decide(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const sv_g1_affine* lhs,
+                        const sv_g1_affine* rhs, size_t n, int form, int num_gpus, int32_t* first_fail) noexcept {
+  SV_GUARD_BEGIN
+  if (n == 0) {
+    sv::set_error("accumulators should not be empty");
+    return SV_ERR_EMPTY;
+  }
+  if (!g2 || !s_g2 || !lhs || !rhs || !first_fail) {
+    sv::set_error("null pointer");
+    return SV_ERR_ARG;
+  }
+  SV_TRY(check_form(form));
+  int ndev = resolve_gpus(num_gpus);
+  if (ndev == 0) return SV_ERR_DEVICE;
+  if ((size_t)ndev > n) ndev = (int)n;
+  size_t per = (n + ndev - 1) / ndev;
+  std::vector<int32_t> ff(ndev, -1);
+  int rc = for_each_device(ndev, [&](int k, int dev) -> int {
+    size_t lo = k * per, hi = std::min(n, lo + per);
+    if (lo >= hi) return SV_OK;
+    size_t m = hi - lo;
+    DevBuf dl, dr;
+    SV_TRY(dl.alloc(dev, m * sizeof(sv_g1_affine)));
+    SV_TRY(dr.alloc(dev, m * sizeof(sv_g1_affine)));
+    SV_HIP(hipMemcpy(dl.p, lhs + lo, m * sizeof(sv_g1_affine), hipMemcpyHostToDevice));
+    SV_HIP(hipMemcpy(dr.p, rhs + lo, m * sizeof(sv_g1_affine), hipMemcpyHostToDevice));
+    int32_t f = -1;
+    SV_TRY(decide_run_device(g2, s_g2, dl.p, dr.p, m, form, dev, nullptr, &f, nullptr, nullptr));
+    ff[k] = f < 0 ? -1 : (int32_t)(lo + f);
+    return SV_OK;
+  });
+  if (rc != SV_OK) return rc;
+  *first_fail = -1;
+  for (int k = 0; k < ndev; k++)
+    if (ff[k] >= 0) {
+      *first_fail = ff[k];
+      break;
+    }
+  return SV_OK;
+  SV_GUARD_END
+}
+
+int sv_bn254_kzg_decide_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const sv_g1_affine* d_lhs,
+                               const sv_g1_affine* d_rhs, size_t n, int form, int device, void* stream,
+                               int32_t* first_fail, int32_t* verdicts, sv_fq12* gt) noexcept {
+  SV_GUARD_BEGIN
+  if (!g2 || !s_g2 || !d_lhs || !d_rhs) {
+    sv::set_error("null pointer");
+    return SV_ERR_ARG;
+  }
+  if (resolve_gpus(0) == 0) return SV_ERR_DEVICE;
+  return decide_run_device(g2, s_g2, d_lhs, d_rhs, n, form, device, (hipStream_t)stream, first_fail,
+                           verdicts, gt);
+  SV_GUARD_END
+}
+
+int sv_bn254_kzg_accumulate(const sv_g1_affine* lhs, const sv_g1_affine* rhs, size_t n, const sv_fe* r,
+                            int form, int num_gpus, sv_g1_affine* out_lhs, sv_g1_affine* out_rhs) noexcept {
+  SV_GUARD_BEGIN
+  (void)num_gpus;  // n is small (one scalar per accumulator): a single device suffices
+  if (n == 0) {
+    sv::set_error("accumulators should not be empty");
+    return SV_ERR_EMPTY;
+  }
+  if (!lhs || !rhs || !r || !out_lhs || !out_rhs) {
+    sv::set_error("null pointer");
+    return SV_ERR_ARG;
+  }
+  SV_TRY(check_form(form));
+  if (resolve_gpus(1) == 0) return SV_ERR_DEVICE;
+  int dev = runtime_device_id(0);
+  DevBuf dbl, dbr, dsc, drr;
+  SV_TRY(dbl.alloc(dev, n * sizeof(sv_g1_affine)));
+  SV_TRY(dbr.alloc(dev, n * sizeof(sv_g1_affine)));
+  SV_TRY(dsc.alloc(dev, n * sizeof(sv_fe)));
+  SV_TRY(drr.alloc(dev, sizeof(sv_fe)));
+  SV_HIP(hipMemcpy(dbl.p, lhs, n * sizeof(sv_g1_affine), hipMemcpyHostToDevice));
+  SV_HIP(hipMemcpy(dbr.p, rhs, n * sizeof(sv_g1_affine), hipMemcpyHostToDevice));
+  SV_HIP(hipMemcpy(drr.p, r, sizeof(sv_fe), hipMemcpyHostToDevice));
+  SV_TRY(powers_device(drr.p, form, n, form, dsc.p, nullptr));
+  SV_HIP(hipDeviceSynchronize());
+  Xyzz a, b;
+  SV_TRY(msm_run_device(dbl.p, dsc.p, n, form, dev, nullptr, &a));
+  SV_TRY(msm_run_device(dbr.p, dsc.p, n, form, dev, nullptr, &b));
+  affine_out(a, form, out_lhs);
+  affine_out(b, form, out_rhs);
+  return SV_OK;
+  SV_GUARD_END
+}
+
+int sv_gen_scalars_device(sv_fe* d_scalars, size_t n, uint64_t seed, uint64_t start, int form, int device,
+                          void* stream) noexcept {
+  SV_GUARD_BEGIN
+  SV_TRY(check_form(form));
+  if (resolve_gpus(0) == 0) return SV_ERR_DEVICE;
+  return gen_scalars_device(d_scalars, n, seed, start, form, device, (hipStream_t)stream);
+  SV_GUARD_END
+}
+
+int sv_gen_bases_device(sv_g1_affine* d_bases, size_t n, uint64_t seed, uint64_t start, int form, int device,
+                        void* stream) noexcept {
+  SV_GUARD_BEGIN
+  SV_TRY(check_form(form));
+  if (resolve_gpus(0) == 0) return SV_ERR_DEVICE;
+  return gen_bases_device(d_bases, n, seed, start, form, device, (hipStream_t)stream);
+  SV_GUARD_END
+}
+
+int sv_msm_last_stats(sv_msm_stats* out) noexcept {
+  SV_GUARD_BEGIN
+  if (!out) return SV_ERR_ARG;
+  return msm_last_stats(out);
+  SV_GUARD_END
+}
+
+}  // extern "C"

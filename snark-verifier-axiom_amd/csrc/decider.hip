@@ -1,0 +1,180 @@
+// KZG decider for BN254 on gfx950: for every accumulator i,
+//     e(lhs_i, g2) * e(rhs_i, -s_g2) == 1
+// Replaces AccumulationDecider::{decide, decide_all} for KzgAs on NativeLoader
+// (snark-verifier/src/pcs/kzg/decider.rs:60-80).
+//
+// The two G2 points are fixed per call, so their Miller-loop line coefficients (88 steps x 3 Fq2
+// each, 33.8 KB for both) are computed once on the host (G2Prepared::from, which the reference
+// redoes inside every decide, decider.rs:64) and uploaded; every accumulator is then one lane:
+// a 2-term multi-Miller loop with sparse 034 line multiplications and the exact final
+// exponentiation, all in registers.  The coefficient reads are lane-uniform (scalar loads).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "curve.hpp"
+#include "decider.hpp"
+#include "runtime.hpp"
+
+namespace sv {
+
+__device__ __forceinline__ G1Aff load_aff_d(const G1Aff* __restrict__ a, uint32_t i, int mont_in) {
+  const uint4* p = reinterpret_cast<const uint4*>(a + i);
+  uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+  G1Aff r;
+  r.x.v[0] = q0.x; r.x.v[1] = q0.y; r.x.v[2] = q0.z; r.x.v[3] = q0.w;
+  r.x.v[4] = q1.x; r.x.v[5] = q1.y; r.x.v[6] = q1.z; r.x.v[7] = q1.w;
+  r.y.v[0] = q2.x; r.y.v[1] = q2.y; r.y.v[2] = q2.z; r.y.v[3] = q2.w;
+  r.y.v[4] = q3.x; r.y.v[5] = q3.y; r.y.v[6] = q3.z; r.y.v[7] = q3.w;
+  if (!mont_in && !r.is_identity()) {
+    r.x = fe_to_mont(r.x);
+    r.y = fe_to_mont(r.y);
+  }
+  return r;
+}
+
+__global__ void __launch_bounds__(64) k_decide(const G1Aff* __restrict__ lhs, const G1Aff* __restrict__ rhs,
+                                                uint32_t n, const LineCoeff* __restrict__ L1,
+                                                const LineCoeff* __restrict__ L2, int mont_in,
+                                                int32_t* __restrict__ verdict, Fq12* __restrict__ gt) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G1Aff p1 = load_aff_d(lhs, i, mont_in);
+  G1Aff p2 = load_aff_d(rhs, i, mont_in);
+  Fq12 f = miller_loop_2(p1, L1, p2, L2);
+  Fq12 e = final_exponentiation(f);
+  verdict[i] = e.is_one() ? 1 : 0;
+  if (gt) gt[i] = e;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host side: prepared-line cache (one entry per device: the deciding key rarely changes).
+// ---------------------------------------------------------------------------------------------
+namespace {
+struct LineCache {
+  std::mutex mu;
+  bool valid = false;
+  unsigned char key[2 * sizeof(G2Aff)];
+  LineCoeff* d_lines = nullptr;  // 2 * ATE_NUM_LINES
+};
+LineCache g_cache[64];
+}  // namespace
+
+static G2Aff g2_from_abi(const sv_g2_affine* q, int mont_in) {
+  G2Aff r;
+  memcpy(&r.x.c0, &q->x.c0, 32);
+  memcpy(&r.x.c1, &q->x.c1, 32);
+  memcpy(&r.y.c0, &q->y.c0, 32);
+  memcpy(&r.y.c1, &q->y.c1, 32);
+  if (!mont_in) {
+    r.x.c0 = fe_to_mont(r.x.c0);
+    r.x.c1 = fe_to_mont(r.x.c1);
+    r.y.c0 = fe_to_mont(r.y.c0);
+    r.y.c1 = fe_to_mont(r.y.c1);
+  }
+  return r;
+}
+
+static bool g2_on_twist(const G2Aff& q) {
+  Fq2 lhs = fq2_sqr(q.y);
+  Fq2 rhs = fq2_sqr(q.x) * q.x + fq2_const(TWIST_B_C0, TWIST_B_C1);
+  return lhs == rhs;
+}
+
+int decider_lines(const sv_g2_affine* g2, const sv_g2_affine* s_g2, int form, int device,
+                  hipStream_t st, const LineCoeff** out) {
+  if (device < 0 || device >= 64) return SV_ERR_ARG;
+  G2Aff q1 = g2_from_abi(g2, form == SV_MONTGOMERY);
+  G2Aff q2 = g2_from_abi(s_g2, form == SV_MONTGOMERY);
+  if (q1.is_identity() || q2.is_identity() || !g2_on_twist(q1) || !g2_on_twist(q2)) {
+    set_error("deciding key G2 point is the identity or not on the twist");
+    return SV_ERR_ARG;
+  }
+  q2.y = -q2.y;  // -s_g2
+  LineCache& c = g_cache[device];
+  std::lock_guard<std::mutex> lk(c.mu);
+  unsigned char key[sizeof c.key];
+  memcpy(key, &q1, sizeof(G2Aff));
+  memcpy(key + sizeof(G2Aff), &q2, sizeof(G2Aff));
+  if (c.valid && memcmp(key, c.key, sizeof key) == 0) {
+    *out = c.d_lines;
+    return SV_OK;
+  }
+  std::vector<LineCoeff> h(2 * ATE_NUM_LINES);
+  g2_prepare(q1, h.data());
+  g2_prepare(q2, h.data() + ATE_NUM_LINES);
+  if (!c.d_lines) SV_HIP(hipMalloc(&c.d_lines, h.size() * sizeof(LineCoeff)));
+  SV_HIP(hipMemcpyAsync(c.d_lines, h.data(), h.size() * sizeof(LineCoeff), hipMemcpyHostToDevice, st));
+  SV_HIP(hipStreamSynchronize(st));
+  memcpy(c.key, key, sizeof key);
+  c.valid = true;
+  *out = c.d_lines;
+  return SV_OK;
+}
+
+int decide_run_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const void* d_lhs,
+                      const void* d_rhs, size_t n, int form, int device, hipStream_t user_stream,
+                      int32_t* first_fail, int32_t* verdicts_host, sv_fq12* gt_host) {
+  if (n == 0) {
+    set_error("accumulators should not be empty");
+    return SV_ERR_EMPTY;
+  }
+  if (form != SV_CANONICAL && form != SV_MONTGOMERY) {
+    set_error("bad form %d", form);
+    return SV_ERR_ARG;
+  }
+  WsLease lease(device, user_stream);
+  if (!lease.ok()) return SV_ERR_DEVICE;
+  Workspace* ws = lease.get();
+  hipStream_t st = ws->stream;
+  const LineCoeff* lines = nullptr;
+  SV_TRY(decider_lines(g2, s_g2, form, device, st, &lines));
+  size_t bytes = Workspace::aligned(n * 4) + (gt_host ? Workspace::aligned(n * sizeof(Fq12)) : 0);
+  SV_TRY(ws->reserve(bytes));
+  SV_TRY(ws->reserve_pinned(n * 4 + 256));
+  int32_t* d_verdict = ws->carve<int32_t>(n);
+  Fq12* d_gt = gt_host ? ws->carve<Fq12>(n) : nullptr;
+  SV_HIP(hipEventRecord(ws->ev[0], st));
+  hipLaunchKernelGGL(k_decide, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st,
+                     reinterpret_cast<const G1Aff*>(d_lhs), reinterpret_cast<const G1Aff*>(d_rhs),
+                     (uint32_t)n, lines, lines + ATE_NUM_LINES, form == SV_MONTGOMERY ? 1 : 0,
+                     d_verdict, d_gt);
+  SV_HIP(hipGetLastError());
+  SV_HIP(hipEventRecord(ws->ev[1], st));
+  int32_t* hv = reinterpret_cast<int32_t*>(ws->pinned);
+  SV_HIP(hipMemcpyAsync(hv, d_verdict, n * 4, hipMemcpyDeviceToHost, st));
+  if (gt_host) {
+    std::vector<Fq12> tmp(n);
+    SV_HIP(hipMemcpyAsync(tmp.data(), d_gt, n * sizeof(Fq12), hipMemcpyDeviceToHost, st));
+    SV_HIP(hipStreamSynchronize(st));
+    for (size_t i = 0; i < n; i++) {
+      const Fq2* c[6] = {&tmp[i].c0.c0, &tmp[i].c0.c1, &tmp[i].c0.c2,
+                         &tmp[i].c1.c0, &tmp[i].c1.c1, &tmp[i].c1.c2};
+      for (int k = 0; k < 6; k++) {
+        Fq a = fe_from_mont(c[k]->c0), b = fe_from_mont(c[k]->c1);
+        memcpy(&gt_host[i].c[k].c0, a.v, 32);
+        memcpy(&gt_host[i].c[k].c1, b.v, 32);
+      }
+    }
+  }
+  SV_HIP(hipStreamSynchronize(st));
+  float ms = 0;
+  hipEventElapsedTime(&ms, ws->ev[0], ws->ev[1]);
+  decider_last_kernel_ms() = ms;
+  int32_t ff = -1;
+  for (size_t i = 0; i < n; i++) {
+    if (verdicts_host) verdicts_host[i] = hv[i];
+    if (ff < 0 && !hv[i]) ff = (int32_t)i;
+  }
+  if (first_fail) *first_fail = ff;
+  return SV_OK;
+}
+
+float& decider_last_kernel_ms() {
+  static thread_local float v = 0;
+  return v;
+}
+
+}  // namespace sv

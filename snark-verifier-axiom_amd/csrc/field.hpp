@@ -1,0 +1,397 @@
+// BN254 field arithmetic for gfx950 (and the host, for the same templates' unit checks).
+//
+// Fq / Fr are 8 x 32-bit little-endian limbs in Montgomery form with R = 2^256 -- byte-for-byte
+// the halo2curves in-memory layout (4 x u64 LE Montgomery), so device buffers can be filled
+// from halo2curves memory with no conversion.  Replaces the halo2curves 0.3.1 Fq/Fr ops that
+// snark-verifier's hot path bottoms out in (reached via snark-verifier/src/util/arithmetic.rs:5-13).
+//
+// Montgomery multiplication is CIOS over 32-bit limbs: every partial product is one
+// v_mad_u64_u32 (32x32+64 -> 64), the instruction gfx950 runs at ~30 per clock per CU
+// (tools/ubench_fpmul.hip; measured 18.2 T/s chip-wide).  Elements are kept fully reduced
+// in [0, p) so equality is bitwise.
+#pragma once
+#include <cstdint>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define SV_HD __host__ __device__ __forceinline__
+#define SV_NOINL __host__ __device__ inline __attribute__((noinline))
+#else
+#define SV_HD inline
+#define SV_NOINL inline
+#endif
+
+#include "bn254_consts.hpp"
+
+namespace sv {
+
+struct FqTag {
+  SV_HD static uint32_t p(int i) { return FQ_P[i]; }
+  SV_HD static uint32_t one(int i) { return FQ_ONE[i]; }
+  SV_HD static uint32_t r2(int i) { return FQ_R2[i]; }
+  static constexpr uint32_t NP0 = FQ_NP0;
+};
+struct FrTag {
+  SV_HD static uint32_t p(int i) { return FR_P[i]; }
+  SV_HD static uint32_t one(int i) { return FR_ONE[i]; }
+  SV_HD static uint32_t r2(int i) { return FR_R2[i]; }
+  static constexpr uint32_t NP0 = FR_NP0;
+};
+
+template <class M>
+struct Fe {
+  uint32_t v[8];
+
+  SV_HD static Fe zero() {
+    Fe r;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = 0;
+    return r;
+  }
+  SV_HD static Fe one() {
+    Fe r;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = M::one(i);
+    return r;
+  }
+  SV_HD static Fe modulus() {
+    Fe r;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = M::p(i);
+    return r;
+  }
+  SV_HD bool is_zero() const {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc |= v[i];
+    return acc == 0;
+  }
+  SV_HD bool operator==(const Fe& o) const {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc |= v[i] ^ o.v[i];
+    return acc == 0;
+  }
+  SV_HD bool operator!=(const Fe& o) const { return !(*this == o); }
+  // true when the raw limbs are < modulus
+  SV_HD bool is_reduced() const {
+    uint64_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      uint64_t s = (uint64_t)v[i] - M::p(i) - br;
+      br = (s >> 63) & 1;
+    }
+    return br == 1;
+  }
+};
+
+template <class M>
+SV_HD Fe<M> fe_select(bool c, const Fe<M>& a, const Fe<M>& b) {
+  Fe<M> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = c ? a.v[i] : b.v[i];
+  return r;
+}
+
+template <class M>
+SV_HD Fe<M> operator+(const Fe<M>& a, const Fe<M>& b) {
+  uint32_t t[8];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t s = (uint64_t)a.v[i] + b.v[i] + c;
+    t[i] = (uint32_t)s;
+    c = s >> 32;
+  }
+  // a + b < 2p < 2^255: no carry out; subtract p when t >= p
+  Fe<M> d;
+  uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t s = (uint64_t)t[i] - M::p(i) - br;
+    d.v[i] = (uint32_t)s;
+    br = (s >> 63) & 1;
+  }
+  Fe<M> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = br ? t[i] : d.v[i];
+  return r;
+}
+
+template <class M>
+SV_HD Fe<M> operator-(const Fe<M>& a, const Fe<M>& b) {
+  uint32_t t[8];
+  uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t s = (uint64_t)a.v[i] - b.v[i] - br;
+    t[i] = (uint32_t)s;
+    br = (s >> 63) & 1;
+  }
+  uint32_t mask = 0u - (uint32_t)br;  // add p back on borrow
+  Fe<M> r;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t s = (uint64_t)t[i] + (M::p(i) & mask) + c;
+    r.v[i] = (uint32_t)s;
+    c = s >> 32;
+  }
+  return r;
+}
+
+template <class M>
+SV_HD Fe<M> operator-(const Fe<M>& a) {
+  return Fe<M>::zero() - a;
+}
+
+template <class M>
+SV_HD Fe<M> fe_dbl(const Fe<M>& a) {
+  return a + a;
+}
+
+// CIOS Montgomery multiplication: r = a * b * 2^-256 mod m.
+template <class M>
+SV_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
+  uint32_t t[10];
+#pragma unroll
+  for (int j = 0; j < 10; j++) t[j] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      uint64_t s = (uint64_t)a.v[j] * b.v[i] + t[j] + c;
+      t[j] = (uint32_t)s;
+      c = s >> 32;
+    }
+    uint64_t s = (uint64_t)t[8] + c;
+    t[8] = (uint32_t)s;
+    t[9] = (uint32_t)(s >> 32);
+    uint32_t m = t[0] * M::NP0;
+    s = (uint64_t)m * M::p(0) + t[0];
+    c = s >> 32;
+#pragma unroll
+    for (int j = 1; j < 8; j++) {
+      s = (uint64_t)m * M::p(j) + t[j] + c;
+      t[j - 1] = (uint32_t)s;
+      c = s >> 32;
+    }
+    s = (uint64_t)t[8] + c;
+    t[7] = (uint32_t)s;
+    t[8] = t[9] + (uint32_t)(s >> 32);
+  }
+  Fe<M> d;
+  uint64_t br = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    uint64_t s = (uint64_t)t[j] - M::p(j) - br;
+    d.v[j] = (uint32_t)s;
+    br = (s >> 63) & 1;
+  }
+  bool ge = (t[8] != 0) || (br == 0);
+  Fe<M> r;
+#pragma unroll
+  for (int j = 0; j < 8; j++) r.v[j] = ge ? d.v[j] : t[j];
+  return r;
+}
+
+template <class M>
+SV_HD Fe<M> fe_sqr(const Fe<M>& a) {
+  return a * a;
+}
+
+template <class M>
+SV_HD Fe<M> fe_to_mont(const Fe<M>& a) {
+  Fe<M> r2;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r2.v[i] = M::r2(i);
+  return a * r2;
+}
+
+template <class M>
+SV_HD Fe<M> fe_from_mont(const Fe<M>& a) {
+  Fe<M> o = Fe<M>::zero();
+  o.v[0] = 1;
+  return a * o;
+}
+
+// a^(m-2): Fermat inverse (0 -> 0).  Exponent bits of m-2 scanned MSB first.
+template <class M>
+SV_NOINL Fe<M> fe_inv(const Fe<M>& a) {
+  uint32_t e[8];
+  uint64_t br = 2;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t s = (uint64_t)M::p(i) - br;
+    e[i] = (uint32_t)s;
+    br = (s >> 63) & 1;
+  }
+  Fe<M> r = Fe<M>::one();
+  for (int i = 7; i >= 0; i--) {
+    for (int b = 31; b >= 0; b--) {
+      r = fe_sqr(r);
+      if ((e[i] >> b) & 1) r = r * a;
+    }
+  }
+  return r;
+}
+
+using Fq = Fe<FqTag>;
+using Fr = Fe<FrTag>;
+
+SV_HD Fq fq_const(const uint32_t (&c)[8]) {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = c[i];
+  return r;
+}
+
+// ------------------------------------------------------------------------------------------
+// Fq2 = Fq[u]/(u^2+1)
+// ------------------------------------------------------------------------------------------
+struct Fq2 {
+  Fq c0, c1;
+  SV_HD static Fq2 zero() { return {Fq::zero(), Fq::zero()}; }
+  SV_HD static Fq2 one() { return {Fq::one(), Fq::zero()}; }
+  SV_HD bool is_zero() const { return c0.is_zero() && c1.is_zero(); }
+  SV_HD bool operator==(const Fq2& o) const { return c0 == o.c0 && c1 == o.c1; }
+};
+
+SV_HD Fq2 operator+(const Fq2& a, const Fq2& b) { return {a.c0 + b.c0, a.c1 + b.c1}; }
+SV_HD Fq2 operator-(const Fq2& a, const Fq2& b) { return {a.c0 - b.c0, a.c1 - b.c1}; }
+SV_HD Fq2 operator-(const Fq2& a) { return {-a.c0, -a.c1}; }
+SV_HD Fq2 operator*(const Fq2& a, const Fq2& b) {
+  Fq t0 = a.c0 * b.c0;
+  Fq t1 = a.c1 * b.c1;
+  Fq t2 = (a.c0 + a.c1) * (b.c0 + b.c1);
+  return {t0 - t1, t2 - t0 - t1};
+}
+SV_HD Fq2 operator*(const Fq2& a, const Fq& s) { return {a.c0 * s, a.c1 * s}; }
+SV_HD Fq2 fq2_sqr(const Fq2& a) {
+  // (a0 + a1)(a0 - a1), 2 a0 a1
+  Fq t = a.c0 * a.c1;
+  return {(a.c0 + a.c1) * (a.c0 - a.c1), t + t};
+}
+SV_HD Fq2 fq2_dbl(const Fq2& a) { return a + a; }
+SV_HD Fq2 fq2_conj(const Fq2& a) { return {a.c0, -a.c1}; }
+SV_HD Fq2 fq2_mul_xi(const Fq2& a) {
+  // (a0 + a1 u)(9 + u) = (9 a0 - a1) + (a0 + 9 a1) u
+  Fq a0_2 = a.c0 + a.c0, a1_2 = a.c1 + a.c1;
+  Fq a0_4 = a0_2 + a0_2, a1_4 = a1_2 + a1_2;
+  Fq a0_8 = a0_4 + a0_4, a1_8 = a1_4 + a1_4;
+  return {a0_8 + a.c0 - a.c1, a1_8 + a.c1 + a.c0};
+}
+SV_NOINL Fq2 fq2_inv(const Fq2& a) {
+  Fq t = fe_inv(fe_sqr(a.c0) + fe_sqr(a.c1));
+  return {a.c0 * t, -(a.c1 * t)};
+}
+SV_HD Fq2 fq2_const(const uint32_t (&c0)[8], const uint32_t (&c1)[8]) {
+  return {fq_const(c0), fq_const(c1)};
+}
+
+// ------------------------------------------------------------------------------------------
+// Fq6 = Fq2[v]/(v^3 - xi),  Fq12 = Fq6[w]/(w^2 - v)
+// ------------------------------------------------------------------------------------------
+struct Fq6 {
+  Fq2 c0, c1, c2;
+  SV_HD static Fq6 zero() { return {Fq2::zero(), Fq2::zero(), Fq2::zero()}; }
+  SV_HD static Fq6 one() { return {Fq2::one(), Fq2::zero(), Fq2::zero()}; }
+  SV_HD bool operator==(const Fq6& o) const { return c0 == o.c0 && c1 == o.c1 && c2 == o.c2; }
+};
+
+SV_HD Fq6 operator+(const Fq6& a, const Fq6& b) { return {a.c0 + b.c0, a.c1 + b.c1, a.c2 + b.c2}; }
+SV_HD Fq6 operator-(const Fq6& a, const Fq6& b) { return {a.c0 - b.c0, a.c1 - b.c1, a.c2 - b.c2}; }
+SV_HD Fq6 operator-(const Fq6& a) { return {-a.c0, -a.c1, -a.c2}; }
+SV_NOINL Fq6 operator*(const Fq6& a, const Fq6& b) {
+  Fq2 t0 = a.c0 * b.c0, t1 = a.c1 * b.c1, t2 = a.c2 * b.c2;
+  Fq2 c0 = t0 + fq2_mul_xi((a.c1 + a.c2) * (b.c1 + b.c2) - t1 - t2);
+  Fq2 c1 = (a.c0 + a.c1) * (b.c0 + b.c1) - t0 - t1 + fq2_mul_xi(t2);
+  Fq2 c2 = (a.c0 + a.c2) * (b.c0 + b.c2) - t0 - t2 + t1;
+  return {c0, c1, c2};
+}
+SV_HD Fq6 fq6_mul_by_v(const Fq6& a) { return {fq2_mul_xi(a.c2), a.c0, a.c1}; }
+SV_NOINL Fq6 fq6_sqr(const Fq6& a) {
+  // CH-SQR2
+  Fq2 s0 = fq2_sqr(a.c0);
+  Fq2 ab = a.c0 * a.c1;
+  Fq2 s1 = fq2_dbl(ab);
+  Fq2 s2 = fq2_sqr(a.c0 - a.c1 + a.c2);
+  Fq2 bc = a.c1 * a.c2;
+  Fq2 s3 = fq2_dbl(bc);
+  Fq2 s4 = fq2_sqr(a.c2);
+  return {s0 + fq2_mul_xi(s3), s1 + fq2_mul_xi(s4), s1 + s2 + s3 - s0 - s4};
+}
+// a * (b0 + b1 v)
+SV_NOINL Fq6 fq6_mul_by_01(const Fq6& a, const Fq2& b0, const Fq2& b1) {
+  Fq2 aa = a.c0 * b0, bb = a.c1 * b1;
+  Fq2 t1 = fq2_mul_xi(a.c2 * b1) + aa;
+  Fq2 t2 = (b0 + b1) * (a.c0 + a.c1) - aa - bb;
+  Fq2 t3 = a.c2 * b0 + bb;
+  return {t1, t2, t3};
+}
+SV_NOINL Fq6 fq6_mul_fq2(const Fq6& a, const Fq2& s) { return {a.c0 * s, a.c1 * s, a.c2 * s}; }
+SV_NOINL Fq6 fq6_inv(const Fq6& a) {
+  Fq2 t0 = fq2_sqr(a.c0) - fq2_mul_xi(a.c1 * a.c2);
+  Fq2 t1 = fq2_mul_xi(fq2_sqr(a.c2)) - a.c0 * a.c1;
+  Fq2 t2 = fq2_sqr(a.c1) - a.c0 * a.c2;
+  Fq2 d = a.c0 * t0 + fq2_mul_xi(a.c2 * t1 + a.c1 * t2);
+  Fq2 di = fq2_inv(d);
+  return {t0 * di, t1 * di, t2 * di};
+}
+
+struct Fq12 {
+  Fq6 c0, c1;
+  SV_HD static Fq12 one() { return {Fq6::one(), Fq6::zero()}; }
+  SV_HD bool operator==(const Fq12& o) const { return c0 == o.c0 && c1 == o.c1; }
+  SV_HD bool is_one() const { return *this == one(); }
+};
+
+SV_NOINL Fq12 operator*(const Fq12& a, const Fq12& b) {
+  Fq6 t0 = a.c0 * b.c0, t1 = a.c1 * b.c1;
+  return {t0 + fq6_mul_by_v(t1), (a.c0 + a.c1) * (b.c0 + b.c1) - t0 - t1};
+}
+SV_NOINL Fq12 fq12_sqr(const Fq12& a) {
+  // complex squaring: c0 = (a0 + a1)(a0 + v a1) - t - v t, c1 = 2t, t = a0 a1
+  Fq6 t = a.c0 * a.c1;
+  Fq6 c0 = (a.c0 + a.c1) * (a.c0 + fq6_mul_by_v(a.c1)) - t - fq6_mul_by_v(t);
+  return {c0, t + t};
+}
+SV_HD Fq12 fq12_conj(const Fq12& a) { return {a.c0, -a.c1}; }
+SV_NOINL Fq12 fq12_inv(const Fq12& a) {
+  Fq6 t = a.c0 * a.c0 - fq6_mul_by_v(a.c1 * a.c1);
+  Fq6 ti = fq6_inv(t);
+  return {a.c0 * ti, -(a.c1 * ti)};
+}
+// f * (c0 + c3 w + c4 v w): the sparse D-type line (positions 0, 3, 4)
+SV_NOINL Fq12 fq12_mul_by_034(const Fq12& f, const Fq2& c0, const Fq2& c3, const Fq2& c4) {
+  Fq6 t0 = fq6_mul_fq2(f.c0, c0);
+  Fq6 t1 = fq6_mul_by_01(f.c1, c3, c4);
+  Fq6 t2 = fq6_mul_by_01(f.c0 + f.c1, c0 + c3, c4) - t0 - t1;
+  return {fq6_mul_by_v(t1) + t0, t2};
+}
+
+// Frobenius^n: coefficient of w^k gets conj^n(g) * GAMMAn_k.
+template <int N>
+SV_NOINL Fq12 fq12_frob(const Fq12& a);
+
+#define SV_G(n, k) fq2_const(GAMMA##n##_##k##_C0, GAMMA##n##_##k##_C1)
+template <>
+SV_NOINL Fq12 fq12_frob<1>(const Fq12& a) {
+  return {{fq2_conj(a.c0.c0), fq2_conj(a.c0.c1) * SV_G(1, 2), fq2_conj(a.c0.c2) * SV_G(1, 4)},
+          {fq2_conj(a.c1.c0) * SV_G(1, 1), fq2_conj(a.c1.c1) * SV_G(1, 3), fq2_conj(a.c1.c2) * SV_G(1, 5)}};
+}
+template <>
+SV_NOINL Fq12 fq12_frob<2>(const Fq12& a) {
+  // GAMMA2_k lie in Fq (c1 = 0)
+  return {{a.c0.c0, a.c0.c1 * SV_G(2, 2).c0, a.c0.c2 * SV_G(2, 4).c0},
+          {a.c1.c0 * SV_G(2, 1).c0, a.c1.c1 * SV_G(2, 3).c0, a.c1.c2 * SV_G(2, 5).c0}};
+}
+template <>
+SV_NOINL Fq12 fq12_frob<3>(const Fq12& a) {
+  return {{fq2_conj(a.c0.c0), fq2_conj(a.c0.c1) * SV_G(3, 2), fq2_conj(a.c0.c2) * SV_G(3, 4)},
+          {fq2_conj(a.c1.c0) * SV_G(3, 1), fq2_conj(a.c1.c1) * SV_G(3, 3), fq2_conj(a.c1.c2) * SV_G(3, 5)}};
+}
+#undef SV_G
+
+}  // namespace sv

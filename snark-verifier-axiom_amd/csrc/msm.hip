@@ -1,0 +1,610 @@
+// Pippenger bucket MSM for BN254 G1 on gfx950.
+//
+// Replaces util::msm::multi_scalar_multiplication (snark-verifier/src/util/msm.rs:238-316) and
+// the naive NativeLoader::multi_scalar_multiplication (snark-verifier/src/loader/native.rs:61-71):
+// same group element out, computed as a signed-digit bucket method.
+//
+// Pipeline (all on one stream, inputs already in HBM):
+//   k_to_mont_bases   (canonical input only) bases -> Montgomery workspace copy
+//   k_digits          scalar -> W signed c-bit digits  dig[w][i] = |d| | sign<<31 (0 = zero digit)
+//   k_hist            per (chunk, window) LDS histogram over the 2^(c-1) buckets -> cnt
+//   k_scan_chunks     per bucket: exclusive prefix over chunks, bucket totals
+//   k_scan_window     per window: exclusive scan of bucket totals (one 1024-thread block)
+//   k_finalize        global bucket offsets gst[], owner bucket of every accumulate chunk
+//   k_scatter         per (chunk, window): LDS cursors, entries sorted by bucket -> ent[]
+//   k_accumulate      each thread sums K consecutive sorted entries (mixed XYZZ adds; perfect
+//                     load balance whatever the digit distribution), complete buckets written
+//                     directly, bucket pieces that cross a thread boundary to pfirst/plast
+//   k_fixup           per bucket: join the pieces of buckets that cross thread boundaries
+//   k_wsum            bucket reduction, step 1: F_w = sum_b (b+1) S_b = sum_j acc_j + L sum_j j T_j
+//                     with running sums over segments of L = 4 buckets (acc_j, T_j per segment)
+//   k_subset_sum      step 2: sum_j j T_j = sum_k 2^k U_k, U_k = sum_{j : bit k of j} T_j; the
+//   k_sum             subset sums U_k and the plain sum of acc_j are independent, so they are all
+//                     tree-reduced together (low serial depth: the tail is latency-bound)
+//   host              Horner over (window, bit) terms (~255 doublings) -> affine, see host_ec.hpp
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "curve.hpp"
+#include "host_ec.hpp"
+#include "msm.hpp"
+#include "runtime.hpp"
+
+namespace sv {
+
+static constexpr int kBlock = 256;
+static constexpr uint32_t kRedL = 4;  // buckets per thread in the running-sum level
+static constexpr int kRedLog = 2;
+
+__device__ __forceinline__ G1Aff load_aff(const G1Aff* __restrict__ a, uint32_t i) {
+  const uint4* p = reinterpret_cast<const uint4*>(a + i);
+  uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+  G1Aff r;
+  r.x.v[0] = q0.x; r.x.v[1] = q0.y; r.x.v[2] = q0.z; r.x.v[3] = q0.w;
+  r.x.v[4] = q1.x; r.x.v[5] = q1.y; r.x.v[6] = q1.z; r.x.v[7] = q1.w;
+  r.y.v[0] = q2.x; r.y.v[1] = q2.y; r.y.v[2] = q2.z; r.y.v[3] = q2.w;
+  r.y.v[4] = q3.x; r.y.v[5] = q3.y; r.y.v[6] = q3.z; r.y.v[7] = q3.w;
+  return r;
+}
+
+__device__ __forceinline__ G1Xyzz load_xyzz(const G1Xyzz* __restrict__ a, uint32_t i) {
+  const uint4* p = reinterpret_cast<const uint4*>(a + i);
+  G1Xyzz r;
+  uint32_t* d = reinterpret_cast<uint32_t*>(&r);
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    uint4 q = p[k];
+    d[4 * k + 0] = q.x; d[4 * k + 1] = q.y; d[4 * k + 2] = q.z; d[4 * k + 3] = q.w;
+  }
+  return r;
+}
+
+__device__ __forceinline__ void store_xyzz(G1Xyzz* __restrict__ a, uint32_t i, const G1Xyzz& v) {
+  uint4* p = reinterpret_cast<uint4*>(a + i);
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(&v);
+#pragma unroll
+  for (int k = 0; k < 8; k++) p[k] = make_uint4(s[4 * k], s[4 * k + 1], s[4 * k + 2], s[4 * k + 3]);
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ void k_to_mont_bases(const G1Aff* __restrict__ in, G1Aff* __restrict__ out, uint32_t n,
+                                uint32_t* __restrict__ err) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G1Aff a = load_aff(in, i);
+  if (!a.x.is_reduced() || !a.y.is_reduced()) atomicOr(err, 1u);
+  G1Aff r;
+  if (a.is_identity()) {
+    r = a;
+  } else {
+    r.x = fe_to_mont(a.x);
+    r.y = fe_to_mont(a.y);
+  }
+  reinterpret_cast<uint4*>(out + i)[0] = make_uint4(r.x.v[0], r.x.v[1], r.x.v[2], r.x.v[3]);
+  reinterpret_cast<uint4*>(out + i)[1] = make_uint4(r.x.v[4], r.x.v[5], r.x.v[6], r.x.v[7]);
+  reinterpret_cast<uint4*>(out + i)[2] = make_uint4(r.y.v[0], r.y.v[1], r.y.v[2], r.y.v[3]);
+  reinterpret_cast<uint4*>(out + i)[3] = make_uint4(r.y.v[4], r.y.v[5], r.y.v[6], r.y.v[7]);
+}
+
+// Signed windows: digit_w = bits[cw, cw+c) + carry, mapped to (-2^(c-1), 2^(c-1)].  W = ceil(255/c)
+// windows so the top digit never carries out (scalars < r < 2^254).
+template <int C>
+__global__ void k_digits(const Fr* __restrict__ scalars, uint32_t n, int mont_in,
+                         uint32_t* __restrict__ dig, uint32_t* __restrict__ err) {
+  constexpr int W = (255 + C - 1) / C;
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4* p = reinterpret_cast<const uint4*>(scalars + i);
+  uint4 q0 = p[0], q1 = p[1];
+  Fr s;
+  s.v[0] = q0.x; s.v[1] = q0.y; s.v[2] = q0.z; s.v[3] = q0.w;
+  s.v[4] = q1.x; s.v[5] = q1.y; s.v[6] = q1.z; s.v[7] = q1.w;
+  if (!s.is_reduced()) atomicOr(err, 2u);
+  if (mont_in) s = fe_from_mont(s);
+  uint32_t carry = 0;
+  const uint32_t half = 1u << (C - 1);
+  const uint32_t mask = (1u << C) - 1;
+#pragma unroll
+  for (int w = 0; w < W; w++) {
+    const int pos = w * C;
+    const int limb = pos >> 5, off = pos & 31;
+    uint32_t lo = limb < 8 ? s.v[limb] : 0;
+    uint32_t hi = (limb + 1) < 8 ? s.v[limb + 1] : 0;
+    uint32_t bits = off ? ((lo >> off) | (hi << (32 - off))) : lo;
+    bits = (bits & mask) + carry;
+    uint32_t out;
+    if (bits > half) {
+      // digit = bits - 2^C <= 0; bits == 2^C (all-ones window + carry) is digit 0 with carry 1
+      const uint32_t mag = (1u << C) - bits;
+      out = mag ? (mag | 0x80000000u) : 0u;
+      carry = 1;
+    } else {
+      out = bits;
+      carry = 0;
+    }
+    dig[(size_t)w * n + i] = out;
+  }
+}
+
+// One block per (chunk, window): LDS histogram of the chunk's digits of this window.
+template <int LOGB>
+__global__ void __launch_bounds__(1024) k_hist(const uint32_t* __restrict__ dig, uint32_t n,
+                                               uint32_t chunk, uint32_t nch,
+                                               uint32_t* __restrict__ cnt) {
+  constexpr uint32_t B = 1u << LOGB;
+  __shared__ uint32_t h[B];
+  const uint32_t ch = blockIdx.x, w = blockIdx.y;
+  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  const uint32_t lo = ch * chunk, hi = min(n, lo + chunk);
+  const uint32_t* d = dig + (size_t)w * n;
+  for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    uint32_t v = d[i];
+    if (v) atomicAdd(&h[(v & 0x7fffffffu) - 1], 1u);
+  }
+  __syncthreads();
+  uint32_t* out = cnt + ((size_t)w * nch + ch) * B;
+  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) out[b] = h[b];
+}
+
+// Per global bucket g = w*B + b: exclusive prefix of cnt over chunks; total -> tot[g].
+__global__ void k_scan_chunks(uint32_t* __restrict__ cnt, uint32_t B, uint32_t W, uint32_t nch,
+                              uint32_t* __restrict__ tot) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= B * W) return;
+  uint32_t w = g / B, b = g % B;
+  uint32_t run = 0;
+  for (uint32_t ch = 0; ch < nch; ch++) {
+    size_t k = ((size_t)w * nch + ch) * B + b;
+    uint32_t c = cnt[k];
+    cnt[k] = run;
+    run += c;
+  }
+  tot[g] = run;
+}
+
+// One 1024-thread block per window: exclusive scan of tot[w*B .. w*B+B) -> bst, total -> wcnt[w].
+__global__ void __launch_bounds__(1024) k_scan_window(const uint32_t* __restrict__ tot, uint32_t B,
+                                                      uint32_t* __restrict__ bst,
+                                                      uint32_t* __restrict__ wcnt) {
+  __shared__ uint32_t part[1024];
+  const uint32_t w = blockIdx.x, tid = threadIdx.x;
+  const uint32_t per = (B + 1023) / 1024;
+  const uint32_t lo = min(B, tid * per), hi = min(B, lo + per);
+  const uint32_t* t = tot + (size_t)w * B;
+  uint32_t s = 0;
+  for (uint32_t b = lo; b < hi; b++) s += t[b];
+  part[tid] = s;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    uint32_t v = tid >= off ? part[tid - off] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[tid] - s;  // exclusive
+  uint32_t* o = bst + (size_t)w * B;
+  for (uint32_t b = lo; b < hi; b++) {
+    o[b] = run;
+    run += t[b];
+  }
+  if (tid == 1023) wcnt[w] = part[1023];
+}
+
+// Global offsets gst[g] (windows concatenated), sentinel gst[W*B] = total entries, and the
+// owner bucket tstart[t] of every accumulate chunk [tK, tK+K).
+__global__ void k_finalize(const uint32_t* __restrict__ bst, const uint32_t* __restrict__ tot,
+                           const uint32_t* __restrict__ wcnt, uint32_t B, uint32_t W, uint32_t K,
+                           uint32_t* __restrict__ gst, uint32_t* __restrict__ tstart) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g > B * W) return;
+  if (g == B * W) {
+    uint32_t m = 0;
+    for (uint32_t w = 0; w < W; w++) m += wcnt[w];
+    gst[g] = m;
+    return;
+  }
+  uint32_t w = g / B;
+  uint32_t base = 0;
+  for (uint32_t k = 0; k < w; k++) base += wcnt[k];
+  uint32_t s = base + bst[g];
+  uint32_t e = s + tot[g];
+  gst[g] = s;
+  for (uint32_t t = (s + K - 1) / K; t * K < e; t++) tstart[t] = g;
+}
+
+template <int LOGB>
+__global__ void __launch_bounds__(1024) k_scatter(const uint32_t* __restrict__ dig, uint32_t n,
+                                                  uint32_t chunk, uint32_t nch,
+                                                  const uint32_t* __restrict__ cnt,
+                                                  const uint32_t* __restrict__ gst,
+                                                  uint32_t* __restrict__ ent) {
+  constexpr uint32_t B = 1u << LOGB;
+  __shared__ uint32_t cur[B];
+  const uint32_t ch = blockIdx.x, w = blockIdx.y;
+  const uint32_t* c = cnt + ((size_t)w * nch + ch) * B;
+  const uint32_t* g = gst + (size_t)w * B;
+  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) cur[b] = g[b] + c[b];
+  __syncthreads();
+  const uint32_t lo = ch * chunk, hi = min(n, lo + chunk);
+  const uint32_t* d = dig + (size_t)w * n;
+  for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    uint32_t v = d[i];
+    if (v) {
+      uint32_t pos = atomicAdd(&cur[(v & 0x7fffffffu) - 1], 1u);
+      ent[pos] = i | (v & 0x80000000u);
+    }
+  }
+}
+
+// Each thread: K consecutive sorted entries.  See file header.
+__global__ void __launch_bounds__(kBlock) k_accumulate(
+    const G1Aff* __restrict__ bases, const uint32_t* __restrict__ ent, const uint32_t* __restrict__ gst,
+    const uint32_t* __restrict__ tstart, uint32_t nbt, uint32_t K, uint32_t T,
+    G1Xyzz* __restrict__ bsum, G1Xyzz* __restrict__ pfirst, G1Xyzz* __restrict__ plast) {
+  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  const uint32_t m = gst[nbt];
+  const uint32_t s0 = t * K;
+  if (s0 >= m) return;
+  const uint32_t e_end = min(s0 + K, m);
+  uint32_t g = tstart[t];
+  uint32_t gs = gst[g], ge = gst[g + 1];
+  uint32_t seg_start = s0;
+  bool first = true;
+  G1Xyzz acc = G1Xyzz::identity();
+  for (uint32_t e = s0; e < e_end; e++) {
+    if (e >= ge) {
+      if (seg_start == gs && e == ge) store_xyzz(bsum, g, acc);
+      else if (first) store_xyzz(pfirst, t, acc);
+      else store_xyzz(plast, t, acc);
+      first = false;
+      do {
+        g++;
+        gs = ge;
+        ge = gst[g + 1];
+      } while (ge <= e);
+      seg_start = e;
+      acc = G1Xyzz::identity();
+    }
+    uint32_t v = ent[e];
+    G1Aff p = load_aff(bases, v & 0x7fffffffu);
+    if (v & 0x80000000u) p.y = -p.y;
+    acc = xyzz_madd_aff(acc, p);
+  }
+  if (seg_start == gs && e_end == ge) store_xyzz(bsum, g, acc);
+  else if (first) store_xyzz(pfirst, t, acc);
+  else store_xyzz(plast, t, acc);
+}
+
+// Per global bucket: empty -> identity; crossing thread boundaries -> join the pieces.
+__global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ gst, uint32_t nbt, uint32_t K,
+                        const G1Xyzz* __restrict__ pfirst, const G1Xyzz* __restrict__ plast,
+                        G1Xyzz* __restrict__ bsum) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nbt) return;
+  uint32_t s = gst[g], e = gst[g + 1];
+  if (s == e) {
+    store_xyzz(bsum, g, G1Xyzz::identity());
+    return;
+  }
+  uint32_t t0 = s / K, t1 = (e - 1) / K;
+  if (t0 == t1) return;
+  G1Xyzz acc = (s == t0 * K) ? load_xyzz(pfirst, t0) : load_xyzz(plast, t0);
+  for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, load_xyzz(pfirst, t));
+  store_xyzz(bsum, g, acc);
+}
+
+// One bucket-reduction level over `groups` groups of N elements, segments of L = kRedL:
+//   acc[g][j] = sum_{i in seg j} (i - jL + base) X[g][i],  tot[g][j] = sum_{i in seg j} X[g][i]
+__global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, uint32_t N, uint32_t J, uint32_t groups, int base,
+                       G1Xyzz* __restrict__ acc_out, G1Xyzz* __restrict__ tot_out) {
+  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= J * groups) return;
+  uint32_t g = tid / J, j = tid % J;
+  const G1Xyzz* x = X + (size_t)g * N;
+  uint32_t lo = j * kRedL;
+  uint32_t hi = min(N, lo + kRedL);
+  G1Xyzz run = G1Xyzz::identity(), acc = G1Xyzz::identity();
+  for (uint32_t i = hi; i-- > lo;) {
+    run = xyzz_add(run, load_xyzz(x, i));
+    if (base || i > lo) acc = xyzz_add(acc, run);
+  }
+  store_xyzz(acc_out, tid, acc);
+  if (tot_out) store_xyzz(tot_out, tid, run);
+}
+
+// Step 2 of the reduction.  Per window w (J segments, H = J/2), NG = 2 + log2(J) groups of H points:
+// q = 0, 1: the two halves of acc[w][*]; q = 2 + k: T[w][j] for the j with bit k set.  Each thread
+// sums F consecutive members of one group: out[(w*NG + q)*O + o].
+__global__ void __launch_bounds__(kBlock) k_subset_sum(const G1Xyzz* __restrict__ acc, const G1Xyzz* __restrict__ tot,
+                                                       uint32_t J, uint32_t logJ, uint32_t W, uint32_t F, uint32_t O,
+                                                       G1Xyzz* __restrict__ out) {
+  const uint32_t NG = 2 + logJ, H = J / 2;
+  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= W * NG * O) return;
+  uint32_t o = tid % O, q = (tid / O) % NG, w = tid / (O * NG);
+  uint32_t lo = o * F, hi = min(H, lo + F);
+  G1Xyzz s = G1Xyzz::identity();
+  for (uint32_t m = lo; m < hi; m++) {
+    G1Xyzz x;
+    if (q < 2) {
+      x = load_xyzz(acc, w * J + q * H + m);
+    } else {
+      uint32_t k = q - 2;
+      uint32_t j = ((m >> k) << (k + 1)) | (1u << k) | (m & ((1u << k) - 1));
+      x = load_xyzz(tot, w * J + j);
+    }
+    s = xyzz_add(s, x);
+  }
+  store_xyzz(out, tid, s);
+}
+
+// Plain sums: out[g][j] = sum of X[g][jF .. jF+F)
+__global__ void __launch_bounds__(kBlock) k_sum(const G1Xyzz* __restrict__ X, uint32_t N, uint32_t F, uint32_t J, uint32_t groups,
+                      G1Xyzz* __restrict__ out) {
+  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= J * groups) return;
+  uint32_t g = tid / J, j = tid % J;
+  const G1Xyzz* x = X + (size_t)g * N;
+  uint32_t lo = j * F, hi = min(N, lo + F);
+  G1Xyzz acc = G1Xyzz::identity();
+  for (uint32_t i = lo; i < hi; i++) acc = xyzz_add(acc, load_xyzz(x, i));
+  store_xyzz(out, tid, acc);
+}
+
+// ---------------------------------------------------------------------------------------------
+// host orchestration
+// ---------------------------------------------------------------------------------------------
+static thread_local sv_msm_stats g_last_stats;
+
+int msm_last_stats(sv_msm_stats* out) {
+  *out = g_last_stats;
+  return SV_OK;
+}
+
+static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+MsmPlan msm_plan(size_t n) {
+  MsmPlan p;
+  int lg = 0;
+  while ((size_t(1) << (lg + 1)) <= n) lg++;
+  int c = lg - 4;
+  if (c < 4) c = 4;
+  if (c > 16) c = 16;
+  p.c = c;
+  p.W = (255 + c - 1) / c;
+  p.B = 1u << (c - 1);
+  p.nbt = p.B * p.W;
+  uint64_t entries = (uint64_t)n * p.W;
+  uint64_t K = entries / (1u << 18);
+  if (K < 4) K = 4;
+  if (K > 32) K = 32;
+  p.K = (uint32_t)K;
+  p.T = cdiv(entries, p.K);
+  uint32_t want_ch = cdiv(256, p.W);
+  uint32_t max_ch = cdiv(n, 4096);
+  p.nch = std::max<uint32_t>(1, std::min(want_ch, max_ch));
+  p.chunk = cdiv(n, p.nch);
+  // reduction: J running-sum segments per window, NG subset groups of H = J/2 points
+  p.J = p.B / kRedL;
+  p.logJ = 0;
+  while ((1u << p.logJ) < p.J) p.logJ++;
+  p.NG = 2 + p.logJ;
+  return p;
+}
+
+#define SV_LAUNCH_LOGB(KERNEL, LOGB, GRID, BLOCK, ...)                          \
+  switch (LOGB) {                                                              \
+    case 3: hipLaunchKernelGGL(KERNEL<3>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 5: hipLaunchKernelGGL(KERNEL<5>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 6: hipLaunchKernelGGL(KERNEL<6>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 7: hipLaunchKernelGGL(KERNEL<7>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 8: hipLaunchKernelGGL(KERNEL<8>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 9: hipLaunchKernelGGL(KERNEL<9>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 10: hipLaunchKernelGGL(KERNEL<10>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 11: hipLaunchKernelGGL(KERNEL<11>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 12: hipLaunchKernelGGL(KERNEL<12>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 13: hipLaunchKernelGGL(KERNEL<13>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 14: hipLaunchKernelGGL(KERNEL<14>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 15: hipLaunchKernelGGL(KERNEL<15>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    default: break;                                                            \
+  }
+
+#define SV_LAUNCH_C(KERNEL, C, GRID, BLOCK, ...)                                \
+  switch (C) {                                                                 \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 5: hipLaunchKernelGGL(KERNEL<5>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 6: hipLaunchKernelGGL(KERNEL<6>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 7: hipLaunchKernelGGL(KERNEL<7>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 8: hipLaunchKernelGGL(KERNEL<8>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 9: hipLaunchKernelGGL(KERNEL<9>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 10: hipLaunchKernelGGL(KERNEL<10>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 11: hipLaunchKernelGGL(KERNEL<11>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 12: hipLaunchKernelGGL(KERNEL<12>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 13: hipLaunchKernelGGL(KERNEL<13>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 14: hipLaunchKernelGGL(KERNEL<14>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 15: hipLaunchKernelGGL(KERNEL<15>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 16: hipLaunchKernelGGL(KERNEL<16>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    default: break;                                                            \
+  }
+
+// Host Horner over (window, group) terms: total = sum_w 2^(c w) [A_lo + A_hi + sum_k 2^(2+k) U_k].
+static host::Xyzz host_combine(const MsmPlan& p, const host::Xyzz* A /* [W][NG] */) {
+  int maxe = (int)(p.c * (p.W - 1) + kRedLog + p.logJ);
+  std::vector<host::Xyzz> byexp(maxe + 1, host::x_identity());
+  for (uint32_t w = 0; w < p.W; w++)
+    for (uint32_t q = 0; q < p.NG; q++) {
+      int e = (int)(p.c * w + (q < 2 ? 0 : kRedLog + (q - 2)));
+      byexp[e] = host::x_add(byexp[e], A[w * p.NG + q]);
+    }
+  host::Xyzz acc = host::x_identity();
+  for (int e = maxe; e >= 0; e--) {
+    acc = host::x_dbl(acc);
+    acc = host::x_add(acc, byexp[e]);
+  }
+  return acc;
+}
+
+int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int form, int device,
+                   hipStream_t user_stream, host::Xyzz* out) {
+  if (n == 0) {
+    set_error("pairs should not be empty");
+    return SV_ERR_EMPTY;
+  }
+  if (n > (size_t(1) << 26)) {
+    set_error("n = %zu exceeds the per-device limit 2^26 (shard across devices/calls)", n);
+    return SV_ERR_LEN;
+  }
+  if (form != SV_CANONICAL && form != SV_MONTGOMERY) {
+    set_error("bad form %d", form);
+    return SV_ERR_ARG;
+  }
+  WsLease lease(device, user_stream);
+  if (!lease.ok()) return SV_ERR_DEVICE;
+  Workspace* ws = lease.get();
+  hipStream_t st = ws->stream;
+  const MsmPlan p = msm_plan(n);
+  const uint64_t entries = (uint64_t)n * p.W;
+
+  // ---- workspace layout
+  size_t bytes = 0;
+  auto add = [&](size_t b) { bytes += Workspace::aligned(b); };
+  bool conv = (form == SV_CANONICAL);
+  if (conv) add(n * sizeof(G1Aff));
+  add(256);                                   // err flag
+  add(entries * 4);                           // dig
+  add((size_t)p.W * p.nch * p.B * 4);         // cnt
+  add((size_t)p.nbt * 4);                     // tot
+  add((size_t)p.nbt * 4);                     // bst
+  add(64 * 4);                                // wcnt
+  add(((size_t)p.nbt + 1) * 4);               // gst
+  add(entries * 4);                           // ent
+  add(((size_t)p.T + 1) * 4);                 // tstart
+  add((size_t)p.T * sizeof(G1Xyzz) * 2);      // pfirst, plast
+  add((size_t)p.nbt * sizeof(G1Xyzz));        // bsum
+  const uint32_t kSubF = 4;
+  const uint32_t O1 = cdiv(p.J / 2, kSubF);   // outputs per group after the first subset launch
+  add((size_t)p.J * p.W * sizeof(G1Xyzz) * 2);         // acc_j, T_j
+  add((size_t)O1 * p.NG * p.W * sizeof(G1Xyzz) * 2);   // sum ping-pong
+  const size_t nfinal = (size_t)p.W * p.NG;
+  SV_TRY(ws->reserve(bytes));
+  SV_TRY(ws->reserve_pinned(nfinal * sizeof(G1Xyzz) + 256));
+
+  const G1Aff* bases = reinterpret_cast<const G1Aff*>(d_bases);
+  G1Aff* bases_m = conv ? ws->carve<G1Aff>(n) : nullptr;
+  uint32_t* err = ws->carve<uint32_t>(64);
+  uint32_t* dig = ws->carve<uint32_t>(entries);
+  uint32_t* cnt = ws->carve<uint32_t>((size_t)p.W * p.nch * p.B);
+  uint32_t* tot = ws->carve<uint32_t>(p.nbt);
+  uint32_t* bst = ws->carve<uint32_t>(p.nbt);
+  uint32_t* wcnt = ws->carve<uint32_t>(64);
+  uint32_t* gst = ws->carve<uint32_t>((size_t)p.nbt + 1);
+  uint32_t* ent = ws->carve<uint32_t>(entries);
+  uint32_t* tstart = ws->carve<uint32_t>((size_t)p.T + 1);
+  G1Xyzz* pfirst = ws->carve<G1Xyzz>(p.T);
+  G1Xyzz* plast = ws->carve<G1Xyzz>(p.T);
+  G1Xyzz* bsum = ws->carve<G1Xyzz>(p.nbt);
+  G1Xyzz* racc = ws->carve<G1Xyzz>((size_t)p.J * p.W);
+  G1Xyzz* rtot = ws->carve<G1Xyzz>((size_t)p.J * p.W);
+  G1Xyzz* ping = ws->carve<G1Xyzz>((size_t)O1 * p.NG * p.W);
+  G1Xyzz* pong = ws->carve<G1Xyzz>((size_t)O1 * p.NG * p.W);
+
+  hipEvent_t* ev = ws->ev;
+  SV_HIP(hipEventRecord(ev[0], st));
+  SV_HIP(hipMemsetAsync(err, 0, 256, st));
+  if (conv) {
+    hipLaunchKernelGGL(k_to_mont_bases, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, st,
+                       bases, bases_m, (uint32_t)n, err);
+    bases = bases_m;
+  }
+  SV_LAUNCH_C(k_digits, p.c, dim3(cdiv(n, kBlock)), dim3(kBlock),
+              reinterpret_cast<const Fr*>(d_scalars), (uint32_t)n, form == SV_MONTGOMERY ? 1 : 0,
+              dig, err);
+  SV_HIP(hipGetLastError());
+  SV_HIP(hipEventRecord(ev[1], st));
+  const int logb = p.c - 1;
+  SV_LAUNCH_LOGB(k_hist, logb, dim3(p.nch, p.W), dim3(1024), dig, (uint32_t)n, p.chunk, p.nch, cnt);
+  hipLaunchKernelGGL(k_scan_chunks, dim3(cdiv(p.nbt, kBlock)), dim3(kBlock), 0, st, cnt, p.B, p.W,
+                     p.nch, tot);
+  hipLaunchKernelGGL(k_scan_window, dim3(p.W), dim3(1024), 0, st, tot, p.B, bst, wcnt);
+  hipLaunchKernelGGL(k_finalize, dim3(cdiv(p.nbt + 1, kBlock)), dim3(kBlock), 0, st, bst, tot, wcnt,
+                     p.B, p.W, p.K, gst, tstart);
+  SV_LAUNCH_LOGB(k_scatter, logb, dim3(p.nch, p.W), dim3(1024), dig, (uint32_t)n, p.chunk, p.nch, cnt,
+                 gst, ent);
+  SV_HIP(hipGetLastError());
+  SV_HIP(hipEventRecord(ev[2], st));
+  hipLaunchKernelGGL(k_accumulate, dim3(cdiv(p.T, kBlock)), dim3(kBlock), 0, st, bases, ent, gst,
+                     tstart, p.nbt, p.K, p.T, bsum, pfirst, plast);
+  SV_HIP(hipGetLastError());
+  SV_HIP(hipEventRecord(ev[3], st));
+  hipLaunchKernelGGL(k_fixup, dim3(cdiv(p.nbt, kBlock)), dim3(kBlock), 0, st, gst, p.nbt, p.K, pfirst,
+                     plast, bsum);
+  SV_HIP(hipEventRecord(ev[4], st));
+  // bucket reduction: running sums over segments of kRedL buckets, then the subset sums
+  hipLaunchKernelGGL(k_wsum, dim3(cdiv((uint64_t)p.J * p.W, kBlock)), dim3(kBlock), 0, st, bsum, p.B, p.J,
+                     p.W, 1, racc, rtot);
+  hipLaunchKernelGGL(k_subset_sum, dim3(cdiv((uint64_t)O1 * p.NG * p.W, kBlock)), dim3(kBlock), 0, st, racc,
+                     rtot, p.J, p.logJ, p.W, kSubF, O1, ping);
+  const G1Xyzz* src = ping;
+  {
+    G1Xyzz* bufs[2] = {pong, ping};
+    int flip = 0;
+    uint32_t N = O1;
+    while (N > 1) {
+      uint32_t F = 4;
+      uint32_t J = cdiv(N, F);
+      G1Xyzz* dst = bufs[flip];
+      hipLaunchKernelGGL(k_sum, dim3(cdiv((uint64_t)J * p.NG * p.W, kBlock)), dim3(kBlock), 0, st, src, N, F, J,
+                         p.NG * p.W, dst);
+      src = dst;
+      flip ^= 1;
+      N = J;
+    }
+  }
+  SV_HIP(hipGetLastError());
+  SV_HIP(hipEventRecord(ev[5], st));
+  SV_HIP(hipMemcpyAsync(ws->pinned, src, nfinal * sizeof(G1Xyzz), hipMemcpyDeviceToHost, st));
+  SV_HIP(hipMemcpyAsync(ws->pinned + nfinal * sizeof(G1Xyzz), err, 4, hipMemcpyDeviceToHost, st));
+  SV_HIP(hipStreamSynchronize(st));
+  uint32_t errv;
+  memcpy(&errv, ws->pinned + nfinal * sizeof(G1Xyzz), 4);
+  if (errv) {
+    set_error("invalid input: %s%s", (errv & 1) ? "base coordinate not reduced mod p; " : "",
+              (errv & 2) ? "scalar not reduced mod r" : "");
+    return SV_ERR_ARG;
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  *out = host_combine(p, reinterpret_cast<const host::Xyzz*>(ws->pinned));
+  auto t1 = std::chrono::steady_clock::now();
+
+  sv_msm_stats& s = g_last_stats;
+  float ms;
+  hipEventElapsedTime(&ms, ev[0], ev[1]);
+  s.digits_ms = ms;
+  hipEventElapsedTime(&ms, ev[1], ev[2]);
+  s.sort_ms = ms;
+  hipEventElapsedTime(&ms, ev[2], ev[3]);
+  s.accumulate_ms = ms;
+  hipEventElapsedTime(&ms, ev[3], ev[4]);
+  s.fixup_ms = ms;
+  hipEventElapsedTime(&ms, ev[4], ev[5]);
+  s.reduce_ms = ms;
+  hipEventElapsedTime(&ms, ev[0], ev[5]);
+  s.host_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
+  s.total_ms = ms + s.host_ms;
+  s.window_bits = p.c;
+  s.num_windows = p.W;
+  s.accumulate_launch_units = p.T;
+  s.entries = entries;
+  return SV_OK;
+}
+
+}  // namespace sv

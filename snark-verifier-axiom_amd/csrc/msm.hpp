@@ -1,0 +1,35 @@
+// Pippenger MSM plan + entry points (see msm.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "../../include/svgpu.h"
+#include "host_ec.hpp"
+
+namespace sv {
+
+struct MsmPlan {
+  int c;            // window bits (signed digits: 2^(c-1) buckets per window)
+  uint32_t W;       // windows = ceil(255 / c)
+  uint32_t B;       // buckets per window
+  uint32_t nbt;     // W * B
+  uint32_t K;       // sorted entries per accumulate thread
+  uint32_t T;       // accumulate threads
+  uint32_t nch;     // point chunks for histogram / scatter
+  uint32_t chunk;   // points per chunk
+  uint32_t J;       // running-sum segments per window (B / 4)
+  uint32_t logJ;    // log2(J)
+  uint32_t NG;      // subset-sum groups per window: 2 + logJ
+};
+
+MsmPlan msm_plan(size_t n);
+
+// Device-resident MSM on `device`; result (XYZZ, Montgomery) on the host.
+int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int form, int device,
+                   hipStream_t stream, host::Xyzz* out);
+
+int msm_last_stats(sv_msm_stats* out);
+
+}  // namespace sv

@@ -1,0 +1,142 @@
+#include "runtime.hpp"
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+
+namespace sv {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+}
+const char* last_error() { return g_err; }
+
+namespace {
+struct DevicePool {
+  int device = 0;
+  std::mutex mu;
+  std::vector<Workspace*> free_list;
+};
+std::once_flag g_once;
+int g_init_rc = SV_ERR_DEVICE;
+std::vector<DevicePool*> g_pools;
+std::mutex g_init_mu;
+}  // namespace
+
+int Workspace::reserve(size_t bytes) {
+  used = 0;
+  if (bytes <= cap) return SV_OK;
+  SV_HIP(hipSetDevice(device));
+  if (buf) {
+    SV_HIP(hipStreamSynchronize(stream));
+    SV_HIP(hipFree(buf));
+    buf = nullptr;
+    cap = 0;
+  }
+  size_t want = bytes + bytes / 8;  // headroom for the next, slightly larger call
+  hipError_t e = hipMalloc(&buf, want);
+  if (e != hipSuccess) {
+    e = hipMalloc(&buf, bytes);
+    want = bytes;
+  }
+  if (e != hipSuccess) {
+    buf = nullptr;
+    set_error("workspace hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+    return SV_ERR_OOM;
+  }
+  cap = want;
+  return SV_OK;
+}
+
+int Workspace::reserve_pinned(size_t bytes) {
+  if (bytes <= pinned_cap) return SV_OK;
+  if (pinned) SV_HIP(hipHostFree(pinned));
+  pinned = nullptr;
+  pinned_cap = 0;
+  SV_HIP(hipHostMalloc(&pinned, bytes, hipHostMallocDefault));
+  pinned_cap = bytes;
+  return SV_OK;
+}
+
+int runtime_init(int num_devices) {
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  if (!g_pools.empty()) return SV_OK;
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count <= 0) {
+    set_error("no usable GPU (hipGetDeviceCount: %s, count=%d)", hipGetErrorString(e), count);
+    return SV_ERR_DEVICE;
+  }
+  if (num_devices > 0 && num_devices < count) count = num_devices;
+  for (int d = 0; d < count; d++) {
+    auto* p = new DevicePool();
+    p->device = d;
+    g_pools.push_back(p);
+  }
+  return SV_OK;
+}
+
+int runtime_device_count() {
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  return (int)g_pools.size();
+}
+
+int runtime_device_id(int idx) { return g_pools[idx]->device; }
+
+static DevicePool* pool_for(int device) {
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  for (auto* p : g_pools)
+    if (p->device == device) return p;
+  return nullptr;
+}
+
+WsLease::WsLease(int device, hipStream_t user_stream) {
+  if (runtime_device_count() == 0 && runtime_init(0) != SV_OK) return;
+  DevicePool* pool = pool_for(device);
+  if (!pool) {
+    set_error("device %d not initialised", device);
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> lk(pool->mu);
+    if (!pool->free_list.empty()) {
+      ws_ = pool->free_list.back();
+      pool->free_list.pop_back();
+    }
+  }
+  if (hipSetDevice(device) != hipSuccess) {
+    set_error("hipSetDevice(%d) failed", device);
+    if (ws_) {
+      std::lock_guard<std::mutex> lk(pool->mu);
+      pool->free_list.push_back(ws_);
+      ws_ = nullptr;
+    }
+    return;
+  }
+  if (!ws_) {
+    ws_ = new Workspace();
+    ws_->device = device;
+    if (hipStreamCreateWithFlags(&ws_->own_stream, hipStreamNonBlocking) != hipSuccess) {
+      set_error("hipStreamCreate failed on device %d", device);
+      delete ws_;
+      ws_ = nullptr;
+      return;
+    }
+    for (auto& ev : ws_->ev) hipEventCreate(&ev);
+  }
+  ws_->stream = user_stream ? user_stream : ws_->own_stream;
+}
+
+WsLease::~WsLease() {
+  if (!ws_) return;
+  DevicePool* pool = pool_for(ws_->device);
+  std::lock_guard<std::mutex> lk(pool->mu);
+  pool->free_list.push_back(ws_);
+}
+
+}  // namespace sv

@@ -1,0 +1,76 @@
+// libsvgpu runtime: per-device stream/workspace pools, error reporting, HIP error plumbing.
+// Calls are re-entrant (SURVEY.md section 8b "Threading"): every call acquires its own
+// Workspace (stream + grow-only device buffer + events) from the device's pool.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/svgpu.h"
+
+namespace sv {
+
+void set_error(const char* fmt, ...);
+const char* last_error();
+
+struct Workspace {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;  // own_stream or a caller-provided stream for this call
+  char* buf = nullptr;
+  size_t cap = 0;
+  size_t used = 0;
+  char* pinned = nullptr;  // host staging
+  size_t pinned_cap = 0;
+  static constexpr int kEvents = 24;
+  hipEvent_t ev[kEvents] = {};
+
+  // carve `bytes` from the device buffer (256-B aligned); call reserve() first
+  template <class T>
+  T* carve(size_t count) {
+    size_t bytes = (count * sizeof(T) + 255) & ~size_t(255);
+    T* p = reinterpret_cast<T*>(buf + used);
+    used += bytes;
+    return p;
+  }
+  static size_t aligned(size_t bytes) { return (bytes + 255) & ~size_t(255); }
+  int reserve(size_t bytes);         // grow-only; resets `used`
+  int reserve_pinned(size_t bytes);  // grow-only pinned host staging
+};
+
+// RAII lease of a per-device workspace; stream override optional.
+class WsLease {
+ public:
+  WsLease(int device, hipStream_t user_stream);
+  ~WsLease();
+  Workspace* get() { return ws_; }
+  bool ok() const { return ws_ != nullptr; }
+
+ private:
+  Workspace* ws_ = nullptr;
+};
+
+int runtime_init(int num_devices);
+int runtime_device_count();
+int runtime_device_id(int idx);  // HIP ordinal of the idx-th initialised device
+
+#define SV_HIP(call)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      ::sv::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #call, hipGetErrorString(e_)); \
+      return e_ == hipErrorOutOfMemory ? SV_ERR_OOM : SV_ERR_DEVICE;                   \
+    }                                                                                  \
+  } while (0)
+
+#define SV_TRY(expr)        \
+  do {                      \
+    int rc_ = (expr);       \
+    if (rc_ != SV_OK) return rc_; \
+  } while (0)
+
+}  // namespace sv

@@ -1,0 +1,86 @@
+"""Device-resident (HBM) entry points over torch tensors.
+
+PyTorch is plumbing here: it owns device memory and the stream; the work is libsvgpu's HIP
+kernels.  Tensors are int64 views of the C-ABI layouts: bases (n, 8), scalars (n, 4).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Tuple
+
+import torch
+
+from . import _lib
+from . import encoding as enc
+
+
+def _stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _dev_index(t: torch.Tensor) -> int:
+    if t.device.type != "cuda":
+        raise _lib.DeviceError("tensor must live on a GPU (cuda/HIP device)")
+    return t.device.index if t.device.index is not None else torch.cuda.current_device()
+
+
+def empty_bases(n: int, device) -> torch.Tensor:
+    return torch.empty((n, 8), dtype=torch.int64, device=device)
+
+
+def empty_scalars(n: int, device) -> torch.Tensor:
+    return torch.empty((n, 4), dtype=torch.int64, device=device)
+
+
+def gen_bases(t: torch.Tensor, seed: int, start: int = 0, form: int = _lib.SV_MONTGOMERY) -> torch.Tensor:
+    d = _dev_index(t)
+    _lib.check(_lib.lib.sv_gen_bases_device(t.data_ptr(), t.shape[0], seed, start, form, d,
+                                            _stream_handle(t.device)), "sv_gen_bases_device")
+    return t
+
+
+def gen_scalars(t: torch.Tensor, seed: int, start: int = 0, form: int = _lib.SV_MONTGOMERY) -> torch.Tensor:
+    d = _dev_index(t)
+    _lib.check(_lib.lib.sv_gen_scalars_device(t.data_ptr(), t.shape[0], seed, start, form, d,
+                                              _stream_handle(t.device)), "sv_gen_scalars_device")
+    return t
+
+
+def msm_partial(bases: torch.Tensor, scalars: torch.Tensor, form: int = _lib.SV_MONTGOMERY) -> Tuple[int, int, int]:
+    """One device's MSM over HBM-resident inputs -> canonical Jacobian (X, Y, Z) on the host."""
+    if bases.shape[0] != scalars.shape[0]:
+        raise ValueError("bases and scalars differ in length")
+    d = _dev_index(bases)
+    out = _lib.sv_g1_jacobian()
+    _lib.check(_lib.lib.sv_bn254_g1_msm_device(bases.data_ptr(), scalars.data_ptr(), bases.shape[0], form, d,
+                                               _stream_handle(bases.device), ctypes.byref(out)),
+               "sv_bn254_g1_msm_device")
+    return enc.jacobian_from_struct(out)
+
+
+def msm(bases: torch.Tensor, scalars: torch.Tensor, form: int = _lib.SV_MONTGOMERY):
+    from .loader import fold_partials
+    return fold_partials([msm_partial(bases, scalars, form)])
+
+
+def last_msm_stats() -> dict:
+    s = _lib.sv_msm_stats()
+    _lib.check(_lib.lib.sv_msm_last_stats(ctypes.byref(s)), "sv_msm_last_stats")
+    return {name: getattr(s, name) for name, _ in s._fields_}
+
+
+def decide(g2, s_g2, lhs: torch.Tensor, rhs: torch.Tensor, form: int = _lib.SV_CANONICAL,
+           want_gt: bool = False) -> Tuple[int, List[int], Optional[List[List[int]]]]:
+    """Decider over HBM-resident accumulators -> (first_fail, verdicts, Gt values or None)."""
+    n = lhs.shape[0]
+    d = _dev_index(lhs)
+    ff = ctypes.c_int32(-2)
+    verdicts = (ctypes.c_int32 * n)()
+    gt = (_lib.sv_fq12 * n)() if want_gt else None
+    g2s, sg2s = enc.g2_struct(g2, form), enc.g2_struct(s_g2, form)
+    _lib.check(_lib.lib.sv_bn254_kzg_decide_device(
+        ctypes.byref(g2s), ctypes.byref(sg2s), lhs.data_ptr(), rhs.data_ptr(), n, form, d,
+        _stream_handle(lhs.device), ctypes.byref(ff), ctypes.cast(verdicts, ctypes.c_void_p),
+        ctypes.cast(gt, ctypes.c_void_p) if gt is not None else None), "sv_bn254_kzg_decide_device")
+    gts = [enc.fq12_from_struct(g) for g in gt] if gt is not None else None
+    return ff.value, list(verdicts), gts

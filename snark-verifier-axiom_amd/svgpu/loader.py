@@ -1,0 +1,69 @@
+"""Host-side mirror of the reference's MSM entry points, executed by libsvgpu on the GPU.
+
+* ``NativeLoader.multi_scalar_multiplication(pairs)`` mirrors
+  ``EcPointLoader::multi_scalar_multiplication`` for ``NativeLoader``
+  (snark-verifier/src/loader/native.rs:61-71): sum of ``base * scalar`` over the pairs, as an
+  affine point; empty input panics with "pairs should not be empty" (native.rs:69).
+* ``multi_scalar_multiplication(scalars, bases)`` mirrors ``util::msm::multi_scalar_multiplication``
+  (snark-verifier/src/util/msm.rs:287-316), whose length check is ``assert_eq!`` (msm.rs:288).
+
+Points are ``(x, y)`` tuples of canonical ints, ``None`` is the identity (halo2curves (0, 0)).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from . import encoding as enc
+
+Point = Optional[Tuple[int, int]]
+
+
+class ReferencePanic(AssertionError):
+    """A condition under which the Rust reference panics."""
+
+
+def msm_arrays(bases: np.ndarray, scalars: np.ndarray, form: int = _lib.SV_CANONICAL, num_gpus: int = 0) -> Point:
+    """MSM over C-ABI-layout host arrays: bases (n, 8) u64, scalars (n, 4) u64."""
+    bases = np.ascontiguousarray(bases, dtype=np.uint64)
+    scalars = np.ascontiguousarray(scalars, dtype=np.uint64)
+    if bases.shape[0] != scalars.shape[0]:
+        raise ReferencePanic("assertion failed: scalars.len() == bases.len()")
+    out = _lib.sv_g1_affine()
+    rc = _lib.lib.sv_bn254_g1_msm(bases.ctypes.data, scalars.ctypes.data, bases.shape[0], form, num_gpus,
+                                  ctypes.byref(out))
+    if rc == _lib.SV_ERR_EMPTY:
+        raise ReferencePanic("pairs should not be empty")
+    _lib.check(rc, "sv_bn254_g1_msm")
+    return enc.g1_from_struct(out, form)
+
+
+def multi_scalar_multiplication(scalars: Sequence[int], bases: Sequence[Point], num_gpus: int = 0) -> Point:
+    if len(scalars) != len(bases):
+        raise ReferencePanic("assertion failed: scalars.len() == bases.len()")
+    return msm_arrays(enc.bases_array(bases), enc.scalars_array(scalars), _lib.SV_CANONICAL, num_gpus)
+
+
+class NativeLoader:
+    """Mirror of snark_verifier::loader::native::NativeLoader (stateless, like the reference's
+    ``lazy_static`` LOADER, native.rs:11-19)."""
+
+    @staticmethod
+    def multi_scalar_multiplication(pairs: Sequence[Tuple[int, Point]], num_gpus: int = 0) -> Point:
+        if len(pairs) == 0:
+            raise ReferencePanic("pairs should not be empty")
+        scalars = [s for s, _ in pairs]
+        bases = [b for _, b in pairs]
+        return multi_scalar_multiplication(scalars, bases, num_gpus)
+
+
+def fold_partials(partials: Sequence[Tuple[int, int, int]], out_form: int = _lib.SV_CANONICAL) -> Point:
+    """Fold canonical Jacobian partials (X, Y, Z) in order -> affine (host-only, no GPU)."""
+    arr = (_lib.sv_g1_jacobian * len(partials))(*[enc.jacobian_struct(*p) for p in partials])
+    out = _lib.sv_g1_affine()
+    _lib.check(_lib.lib.sv_bn254_g1_fold(ctypes.cast(arr, ctypes.c_void_p), len(partials), ctypes.byref(out),
+                                         out_form), "sv_bn254_g1_fold")
+    return enc.g1_from_struct(out, out_form)

@@ -1,0 +1,775 @@
+// C++ CPU restatement of snark-verifier's native hot path -- TEST INFRASTRUCTURE ONLY.
+//
+// Built into oracle/build/liboracle_bn254.so by oracle/cpu/Makefile.  Only tests/, smoke() and
+// bench.py's cpu_baseline leg load it: as the full-size parity checker on the GPU box and as the
+// timed CPU baseline ("kind": "port").  The reference itself (Rust, halo2curves 0.3.1 un-vendored,
+// no cargo in the image) cannot be built here.  Parity of this file is pinned to oracle/bn254.py
+// (tests/test_oracle_cpp.py), which is in turn pinned by the reference's Poseidon KATs (Fr) and by
+// algebraic identities + two independent pairing formulations.
+//
+// Restated functions (reference file:line):
+//   or_msm_naive      NativeLoader::multi_scalar_multiplication   snark-verifier/src/loader/native.rs:61-71
+//   or_msm_pippenger  util::msm::multi_scalar_multiplication      snark-verifier/src/util/msm.rs:238-316
+//                     (window c = ceil(ln n) + 2 :247, byte windows :250-260, Bucket enum :207-236,
+//                      MSB window first :262-281, one chunk per thread + fold :290-310)
+//   or_decide_all     KzgAs decide / decide_all on NativeLoader   snark-verifier/src/pcs/kzg/decider.rs:60-80
+//                     (G2Prepared recomputed inside every decide, as decider.rs:64 does)
+//   or_accumulate     KzgAs::create_proof without blind           snark-verifier/src/pcs/kzg/accumulation.rs:146-195
+//   or_gen_*          SURVEY.md section 8d synthetic inputs (same streams as oracle/bn254.py)
+// Layout: canonical 4 x u64 LE limbs; G1 affine (x, y), identity (0, 0).
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+namespace {
+
+typedef unsigned __int128 u128;
+
+// ------------------------------------------------------------------ prime fields (Montgomery)
+struct Mod {
+  uint64_t p[4];
+  uint64_t np;  // -p^-1 mod 2^64
+  uint64_t r2[4];
+  uint64_t one[4];
+};
+
+const Mod FQ = {{0x3c208c16d87cfd47ull, 0x97816a916871ca8dull, 0xb85045b68181585dull, 0x30644e72e131a029ull},
+                0x87d20782e4866389ull,
+                {0xf32cfc5b538afa89ull, 0xb5e71911d44501fbull, 0x47ab1eff0a417ff6ull, 0x06d89f71cab8351full},
+                {0xd35d438dc58f0d9dull, 0x0a78eb28f5c70b3dull, 0x666ea36f7879462cull, 0x0e0a77c19a07df2full}};
+const Mod FR = {{0x43e1f593f0000001ull, 0x2833e84879b97091ull, 0xb85045b68181585dull, 0x30644e72e131a029ull},
+                0xc2e1f593efffffffull,
+                {0x1bb8e645ae216da7ull, 0x53fe3ab1e35c59e3ull, 0x8c49833d53bb8085ull, 0x0216d0b17f4e44a5ull},
+                {0xac96341c4ffffffbull, 0x36fc76959f60cd29ull, 0x666ea36f7879462eull, 0x0e0a77c19a07df2full}};
+
+struct F {
+  uint64_t l[4];
+};
+
+inline bool geq(const uint64_t* a, const uint64_t* b) {
+  for (int i = 3; i >= 0; i--) {
+    if (a[i] != b[i]) return a[i] > b[i];
+  }
+  return true;
+}
+inline void sub_in(uint64_t* a, const uint64_t* b) {
+  u128 br = 0;
+  for (int i = 0; i < 4; i++) {
+    u128 s = (u128)a[i] - b[i] - br;
+    a[i] = (uint64_t)s;
+    br = (s >> 127) & 1;
+  }
+}
+inline F fadd(const Mod& m, const F& a, const F& b) {
+  F r;
+  u128 c = 0;
+  for (int i = 0; i < 4; i++) {
+    u128 s = (u128)a.l[i] + b.l[i] + c;
+    r.l[i] = (uint64_t)s;
+    c = s >> 64;
+  }
+  if (c || geq(r.l, m.p)) sub_in(r.l, m.p);
+  return r;
+}
+inline F fsub(const Mod& m, const F& a, const F& b) {
+  F r = a;
+  if (!geq(a.l, b.l)) {
+    u128 c = 0;
+    for (int i = 0; i < 4; i++) {
+      u128 s = (u128)r.l[i] + m.p[i] + c;
+      r.l[i] = (uint64_t)s;
+      c = s >> 64;
+    }
+  }
+  sub_in(r.l, b.l);
+  return r;
+}
+inline F fmul(const Mod& m, const F& a, const F& b) {
+  uint64_t t[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 4; i++) {
+    u128 c = 0;
+    for (int j = 0; j < 4; j++) {
+      u128 s = (u128)a.l[j] * b.l[i] + t[j] + c;
+      t[j] = (uint64_t)s;
+      c = s >> 64;
+    }
+    u128 s = (u128)t[4] + c;
+    t[4] = (uint64_t)s;
+    t[5] = (uint64_t)(s >> 64);
+    uint64_t q = t[0] * m.np;
+    s = (u128)q * m.p[0] + t[0];
+    c = s >> 64;
+    for (int j = 1; j < 4; j++) {
+      s = (u128)q * m.p[j] + t[j] + c;
+      t[j - 1] = (uint64_t)s;
+      c = s >> 64;
+    }
+    s = (u128)t[4] + c;
+    t[3] = (uint64_t)s;
+    t[4] = t[5] + (uint64_t)(s >> 64);
+  }
+  F r;
+  memcpy(r.l, t, 32);
+  if (t[4] || geq(r.l, m.p)) sub_in(r.l, m.p);
+  return r;
+}
+inline bool fzero(const F& a) { return (a.l[0] | a.l[1] | a.l[2] | a.l[3]) == 0; }
+inline bool feq(const F& a, const F& b) { return memcmp(a.l, b.l, 32) == 0; }
+inline F fone(const Mod& m) {
+  F r;
+  memcpy(r.l, m.one, 32);
+  return r;
+}
+inline F fto(const Mod& m, const F& a) {
+  F r2;
+  memcpy(r2.l, m.r2, 32);
+  return fmul(m, a, r2);
+}
+inline F ffrom(const Mod& m, const F& a) {
+  F one = {{1, 0, 0, 0}};
+  return fmul(m, a, one);
+}
+inline F fneg(const Mod& m, const F& a) { return fsub(m, F{{0, 0, 0, 0}}, a); }
+F fpow(const Mod& m, const F& a, const uint64_t e[4]) {
+  F r = fone(m);
+  for (int i = 3; i >= 0; i--)
+    for (int b = 63; b >= 0; b--) {
+      r = fmul(m, r, r);
+      if ((e[i] >> b) & 1) r = fmul(m, r, a);
+    }
+  return r;
+}
+F finv(const Mod& m, const F& a) {
+  uint64_t e[4];
+  memcpy(e, m.p, 32);
+  uint64_t two[4] = {2, 0, 0, 0};
+  sub_in(e, two);
+  return fpow(m, a, e);
+}
+
+// Fq shorthands
+inline F qa(const F& a, const F& b) { return fadd(FQ, a, b); }
+inline F qs(const F& a, const F& b) { return fsub(FQ, a, b); }
+inline F qm(const F& a, const F& b) { return fmul(FQ, a, b); }
+inline F qsmall(uint64_t v) { return fto(FQ, F{{v, 0, 0, 0}}); }
+
+// ------------------------------------------------------------------ G1 (Jacobian, Montgomery)
+struct J {
+  F X, Y, Z;
+};
+inline J jid() { return J{fone(FQ), fone(FQ), F{{0, 0, 0, 0}}}; }
+inline bool jis_id(const J& p) { return fzero(p.Z); }
+
+J jdbl(const J& p) {
+  if (jis_id(p) || fzero(p.Y)) return jid();
+  F A = qm(p.X, p.X), B = qm(p.Y, p.Y), C = qm(B, B);
+  F t = qa(p.X, B);
+  F D = qs(qs(qm(t, t), A), C);
+  D = qa(D, D);
+  F E = qa(qa(A, A), A);
+  F Fv = qm(E, E);
+  F X3 = qs(Fv, qa(D, D));
+  F C8 = qa(C, C);
+  C8 = qa(C8, C8);
+  C8 = qa(C8, C8);
+  F Y3 = qs(qm(E, qs(D, X3)), C8);
+  F Z3 = qm(p.Y, p.Z);
+  Z3 = qa(Z3, Z3);
+  return J{X3, Y3, Z3};
+}
+
+J jadd(const J& p, const J& q) {
+  if (jis_id(p)) return q;
+  if (jis_id(q)) return p;
+  F Z1Z1 = qm(p.Z, p.Z), Z2Z2 = qm(q.Z, q.Z);
+  F U1 = qm(p.X, Z2Z2), U2 = qm(q.X, Z1Z1);
+  F S1 = qm(qm(p.Y, q.Z), Z2Z2), S2 = qm(qm(q.Y, p.Z), Z1Z1);
+  if (feq(U1, U2)) {
+    if (feq(S1, S2)) return jdbl(p);
+    return jid();
+  }
+  F H = qs(U2, U1);
+  F I = qa(H, H);
+  I = qm(I, I);
+  F Jv = qm(H, I);
+  F r = qs(S2, S1);
+  r = qa(r, r);
+  F V = qm(U1, I);
+  F X3 = qs(qs(qm(r, r), Jv), qa(V, V));
+  F S1J = qm(S1, Jv);
+  F Y3 = qs(qm(r, qs(V, X3)), qa(S1J, S1J));
+  F zz = qa(p.Z, q.Z);
+  F Z3 = qm(qs(qs(qm(zz, zz), Z1Z1), Z2Z2), H);
+  return J{X3, Y3, Z3};
+}
+
+struct A {  // affine Montgomery, inf flag
+  F x, y;
+  bool inf;
+};
+inline J from_aff(const A& a) { return a.inf ? jid() : J{a.x, a.y, fone(FQ)}; }
+inline J jadd_aff(const J& p, const A& a) { return jadd(p, from_aff(a)); }
+
+A to_aff(const J& p) {
+  if (jis_id(p)) return A{F{{0, 0, 0, 0}}, F{{0, 0, 0, 0}}, true};
+  F zi = finv(FQ, p.Z), zi2 = qm(zi, zi);
+  return A{qm(p.X, zi2), qm(qm(p.Y, zi2), zi), false};
+}
+
+// scalar * base, double-and-add over the canonical bits (halo2curves' group law is the same map)
+J jmul(const A& a, const F& k_canon) {
+  J acc = jid(), base = from_aff(a);
+  for (int i = 3; i >= 0; i--)
+    for (int b = 63; b >= 0; b--) {
+      acc = jdbl(acc);
+      if ((k_canon.l[i] >> b) & 1) acc = jadd(acc, base);
+    }
+  return acc;
+}
+
+A load_aff(const uint64_t* p) {
+  F x, y;
+  memcpy(x.l, p, 32);
+  memcpy(y.l, p + 4, 32);
+  if (fzero(x) && fzero(y)) return A{x, y, true};
+  return A{fto(FQ, x), fto(FQ, y), false};
+}
+void store_aff(const J& p, uint64_t* out) {
+  A a = to_aff(p);
+  if (a.inf) {
+    memset(out, 0, 64);
+    return;
+  }
+  F x = ffrom(FQ, a.x), y = ffrom(FQ, a.y);
+  memcpy(out, x.l, 32);
+  memcpy(out + 4, y.l, 32);
+}
+
+// ------------------------------------------------------------------ Pippenger (msm.rs:238-283)
+enum BKind { B_NONE, B_AFF, B_PROJ };
+struct Bucket {
+  BKind k = B_NONE;
+  A a;
+  J p;
+};
+
+void msm_serial(const uint64_t* scalars, const uint64_t* bases, size_t n, J& result) {
+  // scalars are canonical (== to_repr() bytes, little endian)
+  const size_t window = (size_t)std::ceil(std::log((double)n)) + 2;
+  const size_t num_buckets = ((size_t)1 << window) - 1;
+  const size_t num_bits = 256;
+  std::vector<A> aff(n);
+  for (size_t i = 0; i < n; i++) aff[i] = load_aff(bases + 8 * i);
+  auto windowed = [&](size_t idx, const uint8_t* bytes) -> size_t {
+    size_t skip_bits = idx * window;
+    size_t skip_bytes = skip_bits / 8;
+    uint8_t v[8] = {0};
+    for (size_t k = 0; k < 8 && skip_bytes + k < 32; k++) v[k] = bytes[skip_bytes + k];
+    uint64_t u;
+    memcpy(&u, v, 8);
+    return (size_t)(u >> (skip_bits - skip_bytes * 8)) & num_buckets;
+  };
+  const size_t num_window = (num_bits + window - 1) / window;
+  std::vector<Bucket> buckets(num_buckets);
+  for (size_t idx = num_window; idx-- > 0;) {
+    for (size_t k = 0; k < window; k++) result = jdbl(result);
+    for (auto& b : buckets) b.k = B_NONE;
+    for (size_t i = 0; i < n; i++) {
+      size_t s = windowed(idx, reinterpret_cast<const uint8_t*>(scalars + 4 * i));
+      if (s == 0) continue;
+      Bucket& b = buckets[s - 1];
+      if (b.k == B_NONE) {
+        b.k = B_AFF;
+        b.a = aff[i];
+      } else if (b.k == B_AFF) {
+        b.k = B_PROJ;
+        b.p = jadd_aff(from_aff(b.a), aff[i]);
+      } else {
+        b.p = jadd_aff(b.p, aff[i]);
+      }
+    }
+    J running = jid();
+    for (size_t bi = num_buckets; bi-- > 0;) {
+      const Bucket& b = buckets[bi];
+      if (b.k == B_AFF) running = jadd_aff(running, b.a);
+      else if (b.k == B_PROJ) running = jadd(b.p, running);
+      result = jadd(result, running);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ tower + pairing
+struct F2 {
+  F c0, c1;
+};
+inline F2 f2a(const F2& a, const F2& b) { return {qa(a.c0, b.c0), qa(a.c1, b.c1)}; }
+inline F2 f2s(const F2& a, const F2& b) { return {qs(a.c0, b.c0), qs(a.c1, b.c1)}; }
+inline F2 f2n(const F2& a) { return {fneg(FQ, a.c0), fneg(FQ, a.c1)}; }
+inline F2 f2m(const F2& a, const F2& b) {
+  F t0 = qm(a.c0, b.c0), t1 = qm(a.c1, b.c1);
+  return {qs(t0, t1), qs(qs(qm(qa(a.c0, a.c1), qa(b.c0, b.c1)), t0), t1)};
+}
+inline F2 f2mf(const F2& a, const F& s) { return {qm(a.c0, s), qm(a.c1, s)}; }
+inline F2 f2conj(const F2& a) { return {a.c0, fneg(FQ, a.c1)}; }
+inline F2 f2xi(const F2& a) {
+  F nine = qsmall(9);
+  return {qs(qm(a.c0, nine), a.c1), qa(a.c0, qm(a.c1, nine))};
+}
+inline bool f2zero(const F2& a) { return fzero(a.c0) && fzero(a.c1); }
+F2 f2inv(const F2& a) {
+  F t = finv(FQ, qa(qm(a.c0, a.c0), qm(a.c1, a.c1)));
+  return {qm(a.c0, t), fneg(FQ, qm(a.c1, t))};
+}
+F2 f2pow(F2 a, const std::vector<uint64_t>& e) {  // e little-endian words
+  F2 r = {fone(FQ), F{{0, 0, 0, 0}}};
+  for (size_t i = e.size(); i-- > 0;)
+    for (int b = 63; b >= 0; b--) {
+      r = f2m(r, r);
+      if ((e[i] >> b) & 1) r = f2m(r, a);
+    }
+  return r;
+}
+
+struct F6 {
+  F2 c0, c1, c2;
+};
+inline F6 f6a(const F6& a, const F6& b) { return {f2a(a.c0, b.c0), f2a(a.c1, b.c1), f2a(a.c2, b.c2)}; }
+inline F6 f6s(const F6& a, const F6& b) { return {f2s(a.c0, b.c0), f2s(a.c1, b.c1), f2s(a.c2, b.c2)}; }
+inline F6 f6n(const F6& a) { return {f2n(a.c0), f2n(a.c1), f2n(a.c2)}; }
+F6 f6m(const F6& a, const F6& b) {
+  F2 t0 = f2m(a.c0, b.c0), t1 = f2m(a.c1, b.c1), t2 = f2m(a.c2, b.c2);
+  return {f2a(t0, f2xi(f2s(f2s(f2m(f2a(a.c1, a.c2), f2a(b.c1, b.c2)), t1), t2))),
+          f2a(f2s(f2s(f2m(f2a(a.c0, a.c1), f2a(b.c0, b.c1)), t0), t1), f2xi(t2)),
+          f2a(f2s(f2s(f2m(f2a(a.c0, a.c2), f2a(b.c0, b.c2)), t0), t2), t1)};
+}
+inline F6 f6v(const F6& a) { return {f2xi(a.c2), a.c0, a.c1}; }
+F6 f6inv(const F6& a) {
+  F2 t0 = f2s(f2m(a.c0, a.c0), f2xi(f2m(a.c1, a.c2)));
+  F2 t1 = f2s(f2xi(f2m(a.c2, a.c2)), f2m(a.c0, a.c1));
+  F2 t2 = f2s(f2m(a.c1, a.c1), f2m(a.c0, a.c2));
+  F2 d = f2a(f2m(a.c0, t0), f2xi(f2a(f2m(a.c2, t1), f2m(a.c1, t2))));
+  F2 di = f2inv(d);
+  return {f2m(t0, di), f2m(t1, di), f2m(t2, di)};
+}
+
+struct F12 {
+  F6 c0, c1;
+};
+F12 f12m(const F12& a, const F12& b) {
+  F6 t0 = f6m(a.c0, b.c0), t1 = f6m(a.c1, b.c1);
+  return {f6a(t0, f6v(t1)), f6s(f6s(f6m(f6a(a.c0, a.c1), f6a(b.c0, b.c1)), t0), t1)};
+}
+inline F12 f12conj(const F12& a) { return {a.c0, f6n(a.c1)}; }
+F12 f12inv(const F12& a) {
+  F6 t = f6s(f6m(a.c0, a.c0), f6v(f6m(a.c1, a.c1)));
+  F6 ti = f6inv(t);
+  return {f6m(a.c0, ti), f6n(f6m(a.c1, ti))};
+}
+F12 f12one() {
+  F2 z = {F{{0, 0, 0, 0}}, F{{0, 0, 0, 0}}};
+  F2 o = {fone(FQ), F{{0, 0, 0, 0}}};
+  return {{o, z, z}, {z, z, z}};
+}
+bool f12eq(const F12& a, const F12& b) { return memcmp(&a, &b, sizeof(F12)) == 0; }
+
+// constants derived at init
+struct Consts {
+  F2 xi_p[4][6];  // frobenius^n gammas (index n = 1..3, k = 0..5)
+  F2 twist_b, frob_x, frob_y;
+  F two_inv;
+  std::vector<int> naf;  // 6x+2, LSB first
+};
+Consts* g_c = nullptr;
+
+std::vector<uint64_t> big_from_u128_words(const std::vector<uint64_t>& w) { return w; }
+
+// (p^n - 1) * k / 6 as little-endian words, computed with simple multi-precision
+std::vector<uint64_t> mp_mul_small(const std::vector<uint64_t>& a, uint64_t m) {
+  std::vector<uint64_t> r(a.size() + 1, 0);
+  u128 c = 0;
+  for (size_t i = 0; i < a.size(); i++) {
+    u128 s = (u128)a[i] * m + c;
+    r[i] = (uint64_t)s;
+    c = s >> 64;
+  }
+  r[a.size()] = (uint64_t)c;
+  return r;
+}
+std::vector<uint64_t> mp_mul(const std::vector<uint64_t>& a, const std::vector<uint64_t>& b) {
+  std::vector<uint64_t> r(a.size() + b.size(), 0);
+  for (size_t i = 0; i < a.size(); i++) {
+    u128 c = 0;
+    for (size_t j = 0; j < b.size(); j++) {
+      u128 s = (u128)a[i] * b[j] + r[i + j] + c;
+      r[i + j] = (uint64_t)s;
+      c = s >> 64;
+    }
+    r[i + b.size()] += (uint64_t)c;
+  }
+  return r;
+}
+std::vector<uint64_t> mp_sub_small(std::vector<uint64_t> a, uint64_t m) {
+  u128 br = m;
+  for (size_t i = 0; i < a.size() && br; i++) {
+    u128 s = (u128)a[i] - br;
+    a[i] = (uint64_t)s;
+    br = (s >> 127) & 1;
+  }
+  return a;
+}
+std::vector<uint64_t> mp_div_small(const std::vector<uint64_t>& a, uint64_t d) {
+  std::vector<uint64_t> q(a.size(), 0);
+  u128 rem = 0;
+  for (size_t i = a.size(); i-- > 0;) {
+    u128 cur = (rem << 64) | a[i];
+    q[i] = (uint64_t)(cur / d);
+    rem = cur % d;
+  }
+  return q;
+}
+
+void init_consts() {
+  if (g_c) return;
+  Consts* c = new Consts();
+  F2 xi = {qsmall(9), qsmall(1)};
+  std::vector<uint64_t> p(FQ.p, FQ.p + 4);
+  std::vector<uint64_t> pn = {1};
+  for (int n = 1; n <= 3; n++) {
+    pn = mp_mul(pn, p);
+    std::vector<uint64_t> pm1 = mp_sub_small(pn, 1);
+    for (int k = 0; k < 6; k++) {
+      std::vector<uint64_t> e = mp_div_small(mp_mul_small(pm1, k), 6);
+      c->xi_p[n][k] = f2pow(xi, e);
+    }
+  }
+  c->twist_b = f2mf(f2inv(xi), qsmall(3));
+  std::vector<uint64_t> pm1 = mp_sub_small(p, 1);
+  c->frob_x = f2pow(xi, mp_div_small(pm1, 3));
+  c->frob_y = f2pow(xi, mp_div_small(pm1, 2));
+  c->two_inv = finv(FQ, qsmall(2));
+  // NAF of 6x+2
+  u128 k = (u128)6 * 4965661367192848881ull + 2;
+  while (k > 0) {
+    int d = 0;
+    if (k & 1) {
+      d = 2 - (int)(k & 3);
+      if (d == 1) k -= 1;
+      else k += 1;
+    }
+    c->naf.push_back(d);
+    k >>= 1;
+  }
+  g_c = c;
+}
+
+F12 frob(const F12& a, int n) {
+  const Consts& c = *g_c;
+  auto f = [&](const F2& g, int k) {
+    F2 gg = (n & 1) ? f2conj(g) : g;
+    return k == 0 ? gg : f2m(gg, c.xi_p[n][k]);
+  };
+  return {{f(a.c0.c0, 0), f(a.c0.c1, 2), f(a.c0.c2, 4)}, {f(a.c1.c0, 1), f(a.c1.c1, 3), f(a.c1.c2, 5)}};
+}
+
+struct Line {
+  F2 c0, c3, c4;
+};
+struct G2A {
+  F2 x, y;
+};
+struct G2P {
+  F2 X, Y, Z;
+};
+
+Line dbl_step(G2P& T) {
+  const Consts& c = *g_c;
+  F2 a = f2mf(f2m(T.X, T.Y), c.two_inv);
+  F2 b = f2m(T.Y, T.Y), cc = f2m(T.Z, T.Z);
+  F2 e = f2m(c.twist_b, f2a(f2a(cc, cc), cc));
+  F2 f = f2a(f2a(e, e), e);
+  F2 g = f2mf(f2a(b, f), c.two_inv);
+  F2 yz = f2a(T.Y, T.Z);
+  F2 h = f2s(f2m(yz, yz), f2a(b, cc));
+  F2 i = f2s(e, b);
+  F2 j = f2m(T.X, T.X);
+  F2 e2 = f2m(e, e);
+  T.X = f2m(a, f2s(b, f));
+  T.Y = f2s(f2m(g, g), f2a(f2a(e2, e2), e2));
+  T.Z = f2m(b, h);
+  return {f2n(h), f2a(f2a(j, j), j), i};
+}
+Line add_step(G2P& T, const G2A& Q) {
+  F2 theta = f2s(T.Y, f2m(Q.y, T.Z));
+  F2 lambda = f2s(T.X, f2m(Q.x, T.Z));
+  F2 cc = f2m(theta, theta), d = f2m(lambda, lambda);
+  F2 e = f2m(lambda, d), f = f2m(T.Z, cc), g = f2m(T.X, d);
+  F2 h = f2s(f2a(e, f), f2a(g, g));
+  T.X = f2m(lambda, h);
+  T.Y = f2s(f2m(theta, f2s(g, h)), f2m(e, T.Y));
+  T.Z = f2m(T.Z, e);
+  F2 j = f2s(f2m(theta, Q.x), f2m(lambda, Q.y));
+  return {lambda, f2n(theta), j};
+}
+// G2Prepared::from
+std::vector<Line> prepare(const G2A& Q) {
+  const Consts& c = *g_c;
+  std::vector<Line> out;
+  G2P T = {Q.x, Q.y, {fone(FQ), F{{0, 0, 0, 0}}}};
+  G2A nQ = {Q.x, f2n(Q.y)};
+  for (size_t i = c.naf.size() - 1; i-- > 0;) {
+    out.push_back(dbl_step(T));
+    if (c.naf[i] == 1) out.push_back(add_step(T, Q));
+    else if (c.naf[i] == -1) out.push_back(add_step(T, nQ));
+  }
+  G2A Q1 = {f2m(f2conj(Q.x), c.frob_x), f2m(f2conj(Q.y), c.frob_y)};
+  G2A Q2 = {f2m(f2conj(Q1.x), c.frob_x), f2n(f2m(f2conj(Q1.y), c.frob_y))};
+  out.push_back(add_step(T, Q1));
+  out.push_back(add_step(T, Q2));
+  return out;
+}
+void ell(F12& f, const Line& l, const A& p) {
+  F2 z = {F{{0, 0, 0, 0}}, F{{0, 0, 0, 0}}};
+  F12 line = {{f2mf(l.c0, p.y), z, z}, {f2mf(l.c3, p.x), l.c4, z}};
+  f = f12m(f, line);
+}
+F12 miller(const std::vector<std::pair<A, const std::vector<Line>*>>& terms) {
+  const Consts& c = *g_c;
+  F12 f = f12one();
+  size_t k = 0;
+  size_t L = c.naf.size();
+  for (size_t i = L - 1; i >= 1; i--) {
+    if (i != L - 1) f = f12m(f, f);
+    for (auto& t : terms) ell(f, (*t.second)[k], t.first);
+    k++;
+    if (c.naf[i - 1] != 0) {
+      for (auto& t : terms) ell(f, (*t.second)[k], t.first);
+      k++;
+    }
+  }
+  for (int s = 0; s < 2; s++) {
+    for (auto& t : terms) ell(f, (*t.second)[k], t.first);
+    k++;
+  }
+  return f;
+}
+F12 pow_u64(const F12& a, uint64_t e) {
+  F12 r = f12one();
+  for (int b = 63; b >= 0; b--) {
+    r = f12m(r, r);
+    if ((e >> b) & 1) r = f12m(r, a);
+  }
+  return r;
+}
+F12 final_exp(const F12& f0) {
+  const uint64_t X = 4965661367192848881ull;
+  F12 f = f12m(f12conj(f0), f12inv(f0));
+  f = f12m(frob(f, 2), f);
+  F12 fx = pow_u64(f, X), fx2 = pow_u64(fx, X), fx3 = pow_u64(fx2, X);
+  F12 fx3_36 = pow_u64(fx3, 36);
+  F12 l2 = f12m(pow_u64(fx2, 6), f);
+  F12 l1 = f12m(f12conj(f12m(f12m(fx3_36, pow_u64(fx2, 18)), pow_u64(fx, 12))), f);
+  F12 l0 = f12conj(f12m(f12m(f12m(fx3_36, pow_u64(fx2, 30)), pow_u64(fx, 18)), f12m(f, f)));
+  return f12m(f12m(f12m(l0, frob(l1, 1)), frob(l2, 2)), frob(f, 3));
+}
+
+G2A load_g2(const uint64_t* q) {
+  G2A r;
+  memcpy(r.x.c0.l, q, 32);
+  memcpy(r.x.c1.l, q + 4, 32);
+  memcpy(r.y.c0.l, q + 8, 32);
+  memcpy(r.y.c1.l, q + 12, 32);
+  r.x.c0 = fto(FQ, r.x.c0);
+  r.x.c1 = fto(FQ, r.x.c1);
+  r.y.c0 = fto(FQ, r.y.c0);
+  r.y.c1 = fto(FQ, r.y.c1);
+  return r;
+}
+
+// decide (decider.rs:60-68): lines recomputed per call, like G2Prepared::from in the reference
+F12 decide_gt(const G2A& g2, const G2A& neg_sg2, const A& lhs, const A& rhs) {
+  std::vector<Line> l1 = prepare(g2), l2 = prepare(neg_sg2);
+  std::vector<std::pair<A, const std::vector<Line>*>> terms;
+  if (!lhs.inf) terms.push_back({lhs, &l1});
+  if (!rhs.inf) terms.push_back({rhs, &l2});
+  return final_exp(miller(terms));
+}
+
+// SplitMix64 generator (same streams as oracle/bn254.py)
+struct SM {
+  uint64_t s;
+  uint64_t next() {
+    s += 0x9E3779B97F4A7C15ull;
+    uint64_t z = s;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  }
+};
+F draw254(SM& sm) {
+  F r;
+  for (int k = 0; k < 4; k++) r.l[k] = sm.next();
+  r.l[3] &= (1ull << 62) - 1;
+  return r;
+}
+
+template <class Fn>
+void parallel_for(size_t n, int threads, Fn fn) {
+  if (threads <= 1 || n < 2) {
+    for (size_t i = 0; i < n; i++) fn(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  size_t per = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; t++) {
+    size_t lo = t * per, hi = std::min(n, lo + per);
+    if (lo >= hi) break;
+    th.emplace_back([=] {
+      for (size_t i = lo; i < hi; i++) fn(i);
+    });
+  }
+  for (auto& x : th) x.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+int or_num_threads_default(void) { return (int)std::thread::hardware_concurrency(); }
+
+// NativeLoader MSM: sum_i base_i * scalar_i (canonical in/out).  Returns 1 on empty input (panic).
+int or_msm_naive(const uint64_t* bases, const uint64_t* scalars, size_t n, uint64_t* out) {
+  init_consts();
+  if (n == 0) return 1;
+  J acc = jid();
+  for (size_t i = 0; i < n; i++) {
+    F k;
+    memcpy(k.l, scalars + 4 * i, 32);
+    acc = jadd(acc, jmul(load_aff(bases + 8 * i), k));
+  }
+  store_aff(acc, out);
+  return 0;
+}
+
+// util::msm::multi_scalar_multiplication with `parallel`: threads = rayon current_num_threads.
+int or_msm_pippenger(const uint64_t* bases, const uint64_t* scalars, size_t n, int threads, uint64_t* out) {
+  init_consts();
+  if (threads <= 0) threads = or_num_threads_default();
+  J result = jid();
+  if (n == 0) {
+    store_aff(result, out);
+    return 0;
+  }
+  if (n < (size_t)threads) {
+    msm_serial(scalars, bases, n, result);
+  } else {
+    size_t chunk = (n + threads - 1) / threads;
+    size_t nchunks = (n + chunk - 1) / chunk;
+    std::vector<J> res(nchunks, jid());
+    parallel_for(nchunks, (int)nchunks, [&](size_t c) {
+      size_t lo = c * chunk, hi = std::min(n, lo + chunk);
+      msm_serial(scalars + 4 * lo, bases + 8 * lo, hi - lo, res[c]);
+    });
+    for (auto& r : res) result = jadd(result, r);
+  }
+  store_aff(result, out);
+  return 0;
+}
+
+// decide_all (sequential like decider.rs:75-78 when threads == 1); *first_fail = first failing
+// index or -1.  gt_out (optional, n * 12 * 4 u64 canonical) receives each Gt value.
+int or_decide_all(const uint64_t* g2, const uint64_t* s_g2, const uint64_t* lhs, const uint64_t* rhs, size_t n,
+                  int threads, int32_t* first_fail, uint64_t* gt_out) {
+  init_consts();
+  if (n == 0) return 1;
+  G2A q1 = load_g2(g2), q2 = load_g2(s_g2);
+  q2.y = f2n(q2.y);
+  std::vector<int> ok(n, 0);
+  parallel_for(n, threads, [&](size_t i) {
+    F12 e = decide_gt(q1, q2, load_aff(lhs + 8 * i), load_aff(rhs + 8 * i));
+    ok[i] = f12eq(e, f12one());
+    if (gt_out) {
+      const F2* c[6] = {&e.c0.c0, &e.c0.c1, &e.c0.c2, &e.c1.c0, &e.c1.c1, &e.c1.c2};
+      for (int k = 0; k < 6; k++) {
+        F a = ffrom(FQ, c[k]->c0), b = ffrom(FQ, c[k]->c1);
+        memcpy(gt_out + i * 48 + k * 8, a.l, 32);
+        memcpy(gt_out + i * 48 + k * 8 + 4, b.l, 32);
+      }
+    }
+  });
+  *first_fail = -1;
+  for (size_t i = 0; i < n; i++)
+    if (!ok[i]) {
+      *first_fail = (int32_t)i;
+      break;
+    }
+  return 0;
+}
+
+// KzgAs::create_proof without blind: lhs = sum r^i lhs_i, rhs = sum r^i rhs_i (naive MSMs, as
+// NativeLoader evaluates them).  r canonical.
+int or_accumulate(const uint64_t* lhs, const uint64_t* rhs, size_t n, const uint64_t* r, uint64_t* out_lhs,
+                  uint64_t* out_rhs) {
+  init_consts();
+  if (n == 0) return 1;
+  std::vector<uint64_t> pw(4 * n);
+  F rm;
+  memcpy(rm.l, r, 32);
+  rm = fto(FR, rm);
+  F acc = fone(FR);
+  for (size_t i = 0; i < n; i++) {
+    F c = ffrom(FR, acc);
+    memcpy(&pw[4 * i], c.l, 32);
+    acc = fmul(FR, acc, rm);
+  }
+  or_msm_naive(lhs, pw.data(), n, out_lhs);
+  or_msm_naive(rhs, pw.data(), n, out_rhs);
+  return 0;
+}
+
+void or_gen_scalars(uint64_t seed, uint64_t start, size_t n, uint64_t* out) {
+  for (size_t i = 0; i < n; i++) {
+    SM sm{seed * 0x9E3779B97F4A7C15ull + (start + i) * 0xD1B54A32D192ED03ull};
+    F v;
+    do {
+      v = draw254(sm);
+    } while (geq(v.l, FR.p));
+    memcpy(out + 4 * i, v.l, 32);
+  }
+}
+
+void or_gen_bases(uint64_t seed, uint64_t start, size_t n, int threads, uint64_t* out) {
+  init_consts();
+  // (p+1)/4
+  uint64_t e[4];
+  memcpy(e, FQ.p, 32);
+  {
+    u128 c = 1;
+    for (int i = 0; i < 4; i++) {
+      u128 s = (u128)e[i] + c;
+      e[i] = (uint64_t)s;
+      c = s >> 64;
+    }
+    for (int i = 0; i < 4; i++) e[i] = (e[i] >> 2) | (i < 3 ? (e[i + 1] << 62) : 0);
+  }
+  parallel_for(n, threads, [&](size_t i) {
+    SM sm{seed * 0x9E3779B97F4A7C15ull + (start + i) * 0xD1B54A32D192ED03ull};
+    while (true) {
+      F x = draw254(sm);
+      if (geq(x.l, FQ.p)) continue;
+      F xm = fto(FQ, x);
+      F rhs = qa(qm(qm(xm, xm), xm), qsmall(3));
+      F y = fpow(FQ, rhs, e);
+      if (!feq(qm(y, y), rhs)) continue;
+      uint64_t par = sm.next() & 1;
+      F yc = ffrom(FQ, y);
+      if ((yc.l[0] & 1) != par) yc = fneg(FQ, yc);
+      memcpy(out + 8 * i, x.l, 32);
+      memcpy(out + 8 * i + 4, yc.l, 32);
+      break;
+    }
+  });
+}
+
+}  // extern "C"

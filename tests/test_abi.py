@@ -1,0 +1,80 @@
+"""libsvgpu.so C ABI: loads, exports every prototype in include/svgpu.h, argument/emptiness errors
+without compute, loud failure without a GPU, and the host-only fold."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from oracle import bn254 as b
+
+
+def _header_functions():
+    src = open(os.path.join(ROOT, "include", "svgpu.h")).read()
+    return sorted(set(re.findall(r"\b(sv_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_loads_and_exports_every_header_symbol():
+    import svgpu
+    from svgpu import _lib
+    names = _header_functions()
+    assert len(names) >= 13
+    for n in names:
+        assert hasattr(_lib.lib, n), f"{n} declared in svgpu.h but not exported"
+    assert {p[0] for p in _lib.PROTOTYPES} == set(names), "ctypes prototypes out of sync with svgpu.h"
+    assert "gfx950" in svgpu.version()
+
+
+def test_struct_layouts_match_header():
+    from svgpu import _lib
+    assert ctypes.sizeof(_lib.sv_fe) == 32
+    assert ctypes.sizeof(_lib.sv_g1_affine) == 64
+    assert ctypes.sizeof(_lib.sv_g1_jacobian) == 96
+    assert ctypes.sizeof(_lib.sv_g2_affine) == 128
+    assert ctypes.sizeof(_lib.sv_fq12) == 384
+
+
+def test_empty_inputs_map_to_reference_panics():
+    import svgpu
+    with pytest.raises(svgpu.ReferencePanic, match="pairs should not be empty"):
+        svgpu.NativeLoader.multi_scalar_multiplication([])
+    with pytest.raises(svgpu.ReferencePanic):
+        svgpu.KzgAs.decide_all(svgpu.KzgDecidingKey(b.G1_GEN, b.G2_GEN, b.G2_GEN), [])
+    from svgpu import _lib
+    out = _lib.sv_g1_affine()
+    assert _lib.lib.sv_bn254_g1_msm(None, None, 0, 0, 0, ctypes.byref(out)) == _lib.SV_ERR_EMPTY
+    assert "empty" in _lib.last_error()
+
+
+def test_bad_arguments_rejected():
+    from svgpu import _lib
+    out = _lib.sv_g1_affine()
+    buf = np.zeros(16, np.uint64)
+    assert _lib.lib.sv_bn254_g1_msm(buf.ctypes.data, buf.ctypes.data, 1, 7, 0, ctypes.byref(out)) == _lib.SV_ERR_ARG
+    assert _lib.lib.sv_bn254_g1_msm(None, buf.ctypes.data, 1, 0, 0, ctypes.byref(out)) == _lib.SV_ERR_ARG
+
+
+def test_fold_is_host_only_and_exact():
+    import svgpu
+    pts = [b.g1_mul(b.G1_GEN, k) for k in (3, 5, 7, 11)]
+    z = [2, 3, 1, 5]
+    parts = [(x * zz * zz % b.P, y * zz**3 % b.P, zz) for (x, y), zz in zip(pts, z)]
+    assert svgpu.fold_partials(parts) == b.g1_mul(b.G1_GEN, 26)
+    assert svgpu.fold_partials([(1, 1, 0)]) is None
+    assert svgpu.fold_partials(parts + [(pts[0][0], (-pts[0][1]) % b.P, 1)]) == b.g1_mul(b.G1_GEN, 23)
+    with pytest.raises(svgpu.ArgumentError):
+        svgpu.fold_partials([(b.P, 1, 1)])
+
+
+def _has_gpu():
+    import torch
+    return torch.cuda.is_available()
+
+
+@pytest.mark.skipif(_has_gpu(), reason="checks the no-GPU behaviour")
+def test_compute_without_gpu_fails_loudly():
+    import svgpu
+    with pytest.raises(svgpu.DeviceError):
+        svgpu.multi_scalar_multiplication([1], [b.G1_GEN])

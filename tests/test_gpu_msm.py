@@ -1,0 +1,140 @@
+"""GPU MSM parity through the C ABI (libsvgpu's HIP kernels) against the oracles."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import pt
+from oracle import bn254 as b
+
+pytestmark = pytest.mark.gpu
+
+
+def _to_pt(row):
+    return b.g1_from_bytes(np.asarray(row, dtype=np.uint64).tobytes())
+
+
+def _golden_inputs(c, oracle_cpp):
+    from svgpu import encoding as enc
+    if "scalars" in c:
+        return enc.bases_array([pt(p) for p in c["bases"]]), enc.scalars_array([int(s, 16) for s in c["scalars"]])
+    return (oracle_cpp.gen_bases(c["seeds"]["bases"], c["n"]), oracle_cpp.gen_scalars(c["seeds"]["scalars"], c["n"]))
+
+
+def test_golden_host_api_both_forms(gpu, golden_msm, oracle_cpp):
+    import svgpu
+    from svgpu import encoding as enc
+    for c in golden_msm["cases"]:
+        B, S = _golden_inputs(c, oracle_cpp)
+        exp = pt(c["expected"])
+        assert svgpu.msm_arrays(B, S, svgpu.SV_CANONICAL) == exp, c["name"]
+        pts = [enc.g1_from_limbs(r) for r in B]
+        sc = [enc.limbs_to_int(r) for r in S]
+        Bm, Sm = enc.bases_array(pts, svgpu.SV_MONTGOMERY), enc.scalars_array(sc, svgpu.SV_MONTGOMERY)
+        assert svgpu.msm_arrays(Bm, Sm, svgpu.SV_MONTGOMERY) == exp, c["name"]
+
+
+def test_native_loader_mirror(gpu, golden_msm):
+    import svgpu
+    c = next(c for c in golden_msm["cases"] if c["name"] == "mixed_edges")
+    pairs = [(int(s, 16), pt(p)) for s, p in zip(c["scalars"], c["bases"])]
+    assert svgpu.NativeLoader.multi_scalar_multiplication(pairs) == pt(c["expected"])
+
+
+def test_device_generators_match_oracle(gpu, oracle_cpp):
+    import svgpu
+    from svgpu import device as dv
+    n = 5000
+    for form in (svgpu.SV_CANONICAL, svgpu.SV_MONTGOMERY):
+        Bd = dv.gen_bases(dv.empty_bases(n, gpu), b.SEED_BASES, 123, form)
+        Sd = dv.gen_scalars(dv.empty_scalars(n, gpu), b.SEED_SCALARS, 123, form)
+        torch.cuda.synchronize()
+        Bh = Bd.cpu().numpy().view(np.uint64)
+        Sh = Sd.cpu().numpy().view(np.uint64)
+        Bo = oracle_cpp.gen_bases(b.SEED_BASES, n, start=123)
+        So = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=123)
+        if form == svgpu.SV_MONTGOMERY:
+            from svgpu import encoding as enc
+            Bh = enc.bases_array([enc.g1_from_limbs(r, form) for r in Bh])
+            Sh = enc.scalars_array([enc._from_form(enc.limbs_to_int(r), b.R, form) for r in Sh])
+        assert (Bh == Bo).all() and (Sh == So).all()
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 63, 64, 65, 1000, 4095, 4096, 65537])
+def test_random_sizes_vs_cpp_pippenger(gpu, oracle_cpp, n):
+    from svgpu import device as dv
+    import svgpu
+    B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=7 * n)
+    S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=7 * n)
+    exp = _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
+    Bd = torch.from_numpy(B.view(np.int64)).to(gpu)
+    Sd = torch.from_numpy(S.view(np.int64)).to(gpu)
+    assert dv.msm(Bd, Sd, svgpu.SV_CANONICAL) == exp
+
+
+def test_adversarial_single_bucket(gpu, oracle_cpp):
+    """All scalars equal: every window's digits land in ONE bucket (maximal bucket skew)."""
+    import svgpu
+    n = 20000
+    B = oracle_cpp.gen_bases(b.SEED_BASES, n)
+    S = np.tile(np.array([0xDEADBEEFCAFEBABE, 0x1234, 0, 0x0FFF], np.uint64), (n, 1))
+    assert svgpu.msm_arrays(B, S) == _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
+
+
+def test_repeated_and_cancelling_points(gpu, oracle_cpp):
+    import svgpu
+    n = 3000
+    B = oracle_cpp.gen_bases(b.SEED_BASES, 10)
+    B = np.concatenate([B] * (n // 10))
+    S = oracle_cpp.gen_scalars(b.SEED_SCALARS, 10)
+    S = np.concatenate([S] * (n // 10))
+    exp = _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
+    assert svgpu.msm_arrays(B, S) == exp
+    # P and -P with equal scalars cancel to the identity
+    from svgpu import encoding as enc
+    pts = [enc.g1_from_limbs(r) for r in B[:10]]
+    negs = [b.g1_neg(p) for p in pts]
+    allp = enc.bases_array(pts + negs)
+    sc = np.concatenate([S[:10], S[:10]])
+    assert svgpu.msm_arrays(allp, sc) is None
+
+
+def test_invalid_scalar_rejected(gpu):
+    import svgpu
+    from svgpu import encoding as enc
+    B = enc.bases_array([b.G1_GEN])
+    S = enc.ints_to_limbs([b.R])
+    with pytest.raises(svgpu.ArgumentError):
+        svgpu.msm_arrays(B, S)
+
+
+def test_full_size_2_20_parity_and_properties(gpu, oracle_cpp):
+    """Config 2 size: GPU == C++ Pippenger at 2^20; linearity and shard-additivity properties."""
+    import svgpu
+    from svgpu import device as dv, encoding as enc
+    n = 1 << 20
+    Bd = dv.gen_bases(dv.empty_bases(n, gpu), b.SEED_BASES, 0, svgpu.SV_MONTGOMERY)
+    Sd = dv.gen_scalars(dv.empty_scalars(n, gpu), b.SEED_SCALARS, 0, svgpu.SV_MONTGOMERY)
+    got = dv.msm(Bd, Sd, svgpu.SV_MONTGOMERY)
+    B = oracle_cpp.gen_bases(b.SEED_BASES, n)
+    S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n)
+    assert got == _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
+    # shard additivity: two halves folded == whole
+    h = n // 2
+    p1 = dv.msm_partial(Bd[:h], Sd[:h], svgpu.SV_MONTGOMERY)
+    p2 = dv.msm_partial(Bd[h:], Sd[h:], svgpu.SV_MONTGOMERY)
+    assert svgpu.fold_partials([p1, p2]) == got
+    # linearity in the scalars: MSM(2 s) == 2 MSM(s) (scalars doubled mod r on the host)
+    S2 = enc.scalars_array([(2 * enc.limbs_to_int(r)) % b.R for r in S[:4096]])
+    g1 = svgpu.msm_arrays(B[:4096], S[:4096])
+    g2 = svgpu.msm_arrays(B[:4096], S2)
+    assert g2 == b.g1_add(g1, g1)
+
+
+def test_multi_device_host_api_consistent(gpu, oracle_cpp):
+    import svgpu
+    n = 10000
+    B = oracle_cpp.gen_bases(b.SEED_BASES, n)
+    S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n)
+    exp = _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
+    for g in (0, 1, 2):
+        assert svgpu.msm_arrays(B, S, svgpu.SV_CANONICAL, num_gpus=g) == exp

@@ -1,0 +1,38 @@
+"""Host-side encodings of the reference interface mirror (no GPU)."""
+import numpy as np
+import pytest
+
+from oracle import bn254 as b
+
+
+def test_roundtrip_forms():
+    from svgpu import encoding as enc, SV_CANONICAL, SV_MONTGOMERY
+    pts = [b.G1_GEN, None, b.g1_mul(b.G1_GEN, 77)]
+    for form in (SV_CANONICAL, SV_MONTGOMERY):
+        arr = enc.bases_array(pts, form)
+        assert arr.shape == (3, 8)
+        assert [enc.g1_from_limbs(r, form) for r in arr] == pts
+    assert (enc.bases_array([None])[0] == 0).all()
+    m = enc.bases_array([b.G1_GEN], SV_MONTGOMERY)[0]
+    assert enc.limbs_to_int(m[:4]) == b.to_mont(1)
+
+
+def test_scalar_validation():
+    from svgpu import encoding as enc
+    with pytest.raises(ValueError):
+        enc.scalars_array([b.R])
+    a = enc.scalars_array([0, 1, b.R - 1])
+    assert [enc.limbs_to_int(r) for r in a] == [0, 1, b.R - 1]
+
+
+def test_halo2curves_layout_is_little_endian_u64_limbs():
+    from svgpu import encoding as enc
+    x = 0x0102030405060708_1112131415161718_2122232425262728_3132333435363738
+    row = enc.ints_to_limbs([x])[0]
+    assert row[0] == 0x3132333435363738 and row[3] == 0x0102030405060708
+
+
+def test_length_mismatch_panics():
+    import svgpu
+    with pytest.raises(svgpu.ReferencePanic):
+        svgpu.multi_scalar_multiplication([1, 2], [b.G1_GEN])

@@ -1,0 +1,51 @@
+"""Summarise a rocprofv3 run (tools/profile_*.sh) into profiles/: kernel-stats table + PMC HBM bytes.
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  gfx950 correction (MI355X_MICROARCH.md, HBM):
+FETCH_SIZE reads exactly half the bytes of wide (16 B/lane) coalesced streaming reads; other access
+widths are uncalibrated, so both the raw and the x2-corrected read figures are recorded.
+usage: python3 tools/summarize_profile.py gpurun_out/prof profiles r01
+"""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+src, dst, tag = sys.argv[1], sys.argv[2], sys.argv[3]
+os.makedirs(dst, exist_ok=True)
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").replace("sv::", "")
+
+
+rows = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+total = sum(float(r["TotalDurationNs"]) for r in rows)
+lines = [f"# rocprofv3 --kernel-trace --stats, bench.py --steps 10 --warmup 2 ({tag})", "",
+         "| kernel | calls | avg us | total ms | % |", "|---|---|---|---|---|"]
+for r in rows:
+    lines.append("| %s | %s | %.1f | %.3f | %.1f |" % (short(r["Name"]), r["Calls"], float(r["AverageNs"]) / 1e3,
+                                                       float(r["TotalDurationNs"]) / 1e6, float(r["Percentage"])))
+pmc = {}
+for counter, sub in (("FETCH_SIZE", "pmc_fetch"), ("WRITE_SIZE", "pmc_write")):
+    acc = defaultdict(list)
+    for r in csv.DictReader(open(os.path.join(src, sub, "run_counter_collection.csv"))):
+        acc[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+    pmc[counter] = {k: sum(v) / len(v) for k, v in acc.items()}
+lines += ["", "## HBM traffic per launch (PMC, separate passes)", "",
+          "| kernel | FETCH_SIZE KiB (raw) | reads x2 corrected MB | WRITE_SIZE KiB | MB total (corrected) |",
+          "|---|---|---|---|---|"]
+for k in sorted(pmc["FETCH_SIZE"], key=lambda k: -pmc["FETCH_SIZE"][k]):
+    f = pmc["FETCH_SIZE"][k]
+    w = pmc["WRITE_SIZE"].get(k, 0.0)
+    lines.append("| %s | %.0f | %.1f | %.0f | %.1f |" % (k, f, 2 * f * 1024 / 1e6, w, (2 * f + w) * 1024 / 1e6))
+open(os.path.join(dst, f"{tag}_kernel_stats.md"), "w").write("\n".join(lines) + "\n")
+acc_f = pmc["FETCH_SIZE"].get("k_accumulate")
+acc_w = pmc["WRITE_SIZE"].get("k_accumulate")
+if acc_f is not None:
+    json.dump({"kernel": "k_accumulate", "source": f"profiles/{tag}_kernel_stats.md",
+               "fetch_kib_raw": acc_f, "write_kib": acc_w,
+               "hbm_bytes_per_launch": (2 * acc_f + (acc_w or 0)) * 1024,
+               "correction": "reads doubled per MI355X_MICROARCH.md HBM note (uncalibrated for 16-B gathers)"},
+              open(os.path.join(dst, "pmc_accumulate.json"), "w"), indent=1)
+print("\n".join(lines))

@@ -5,10 +5,11 @@
 // from halo2curves memory with no conversion.  Replaces the halo2curves 0.3.1 Fq/Fr ops that
 // snark-verifier's hot path bottoms out in (reached via snark-verifier/src/util/arithmetic.rs:5-13).
 //
-// Montgomery multiplication is CIOS over 32-bit limbs: every partial product is one
-// v_mad_u64_u32 (32x32+64 -> 64), the instruction gfx950 runs at ~30 per clock per CU
-// (tools/ubench_fpmul.hip; measured 18.2 T/s chip-wide).  Elements are kept fully reduced
-// in [0, p) so equality is bitwise.
+// Montgomery multiplication on the device is finely-integrated product scanning over 32-bit limbs:
+// every partial product is one v_mad_u64_u32 (32x32+64 -> 64, ~30 per clock per CU, measured
+// 18.2 T/s chip-wide by tools/ubench_fpmul.hip) whose carry-out feeds a v_addc -- 128 products,
+// 130 G mul/s (tools/ubench_mulvar).  The host build of the same templates uses portable CIOS.
+// Elements are kept fully reduced in [0, p) so equality is bitwise.
 #pragma once
 #include <cstdint>
 
@@ -150,7 +151,62 @@ SV_HD Fe<M> fe_dbl(const Fe<M>& a) {
   return a + a;
 }
 
-// CIOS Montgomery multiplication: r = a * b * 2^-256 mod m.
+#if defined(__HIP_DEVICE_COMPILE__)
+// acc (64 bit) += a * b with the carry out of v_mad_u64_u32 collected in ovf: two VALU
+// instructions per partial product and no re-packing of 64-bit addends (the compiler's CIOS
+// lowering spends ~2.3 v_mov per product on that; tools/ubench_mulvar: 99.6 -> 130 G mul/s).
+__device__ __forceinline__ void mac_carry(uint64_t& acc, uint32_t& ovf, uint32_t a, uint32_t b) {
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+      : "+v"(acc), "+v"(ovf)
+      : "v"(a), "v"(b)
+      : "vcc");
+}
+
+// Montgomery multiplication by finely integrated product scanning: column k accumulates
+// a_i b_{k-i} and m_i p_{k-i} in (acc, ovf); for k < 8 the column's low word fixes m_k.
+template <class M>
+SV_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
+  uint32_t m[8], t[8];
+  uint64_t acc = 0;
+  uint32_t ovf = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < 8) mac_carry(acc, ovf, a.v[i], b.v[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < 8) mac_carry(acc, ovf, m[i], M::p(j));
+    }
+    if (k < 8) {
+      m[k] = (uint32_t)acc * M::NP0;
+      mac_carry(acc, ovf, m[k], M::p(0));
+    } else {
+      t[k - 8] = (uint32_t)acc;
+    }
+    acc = (acc >> 32) | ((uint64_t)ovf << 32);
+    ovf = 0;
+  }
+  const uint32_t top = (uint32_t)acc;
+  Fe<M> d;
+  uint64_t br = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    uint64_t s = (uint64_t)t[j] - M::p(j) - br;
+    d.v[j] = (uint32_t)s;
+    br = (s >> 63) & 1;
+  }
+  const bool ge = (top != 0) || (br == 0);
+  Fe<M> r;
+#pragma unroll
+  for (int j = 0; j < 8; j++) r.v[j] = ge ? d.v[j] : t[j];
+  return r;
+}
+#else
+// CIOS Montgomery multiplication (host build of the same templates): r = a * b * 2^-256 mod m.
 template <class M>
 SV_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
   uint32_t t[10];
@@ -195,6 +251,7 @@ SV_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
   for (int j = 0; j < 8; j++) r.v[j] = ge ? d.v[j] : t[j];
   return r;
 }
+#endif
 
 template <class M>
 SV_HD Fe<M> fe_sqr(const Fe<M>& a) {

@@ -18,9 +18,9 @@
 //   k_fixup           per bucket: join the pieces of buckets that cross thread boundaries
 //   k_wsum            bucket reduction, step 1: F_w = sum_b (b+1) S_b = sum_j acc_j + L sum_j j T_j
 //                     with running sums over segments of L = 4 buckets (acc_j, T_j per segment)
-//   k_subset_sum      step 2: sum_j j T_j = sum_k 2^k U_k, U_k = sum_{j : bit k of j} T_j; the
-//   k_sum             subset sums U_k and the plain sum of acc_j are independent, so they are all
-//                     tree-reduced together (low serial depth: the tail is latency-bound)
+//   k_group_sum       step 2: sum_j j T_j = sum_k 2^k U_k, U_k = sum_{j : bit k of j} T_j; the
+//                     subset sums U_k and the plain sum of acc_j are independent, so each is one
+//                     block-level tree reduction in LDS (low serial depth: the tail is latency-bound)
 //   host              Horner over (window, bit) terms (~255 doublings) -> affine, see host_ec.hpp
 #include <hip/hip_runtime.h>
 
@@ -28,6 +28,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -283,10 +284,14 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
   else store_xyzz(plast, t, acc);
 }
 
-// Per global bucket: empty -> identity; crossing thread boundaries -> join the pieces.
+// Per global bucket: empty -> identity; crossing thread boundaries -> join the pieces.  A bucket
+// spanning more than kFixSerial threads (skewed digits: all-equal scalars, a short top window) is
+// queued for k_fixup_heavy instead of being walked serially.
+static constexpr uint32_t kFixSerial = 8;
 __global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ gst, uint32_t nbt, uint32_t K,
-                        const G1Xyzz* __restrict__ pfirst, const G1Xyzz* __restrict__ plast,
-                        G1Xyzz* __restrict__ bsum) {
+                                                  const G1Xyzz* __restrict__ pfirst, const G1Xyzz* __restrict__ plast,
+                                                  G1Xyzz* __restrict__ bsum, uint32_t* __restrict__ heavy,
+                                                  uint32_t* __restrict__ nheavy) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= nbt) return;
   uint32_t s = gst[g], e = gst[g + 1];
@@ -296,9 +301,43 @@ __global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ g
   }
   uint32_t t0 = s / K, t1 = (e - 1) / K;
   if (t0 == t1) return;
+  if (t1 - t0 > kFixSerial) {
+    heavy[atomicAdd(nheavy, 1u)] = g;
+    return;
+  }
   G1Xyzz acc = (s == t0 * K) ? load_xyzz(pfirst, t0) : load_xyzz(plast, t0);
   for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, load_xyzz(pfirst, t));
   store_xyzz(bsum, g, acc);
+}
+
+// Heavy buckets: one block per queued bucket (grid-stride over the queue), strided partial sums of
+// the per-thread pieces + LDS tree.
+__global__ void __launch_bounds__(kBlock) k_fixup_heavy(const uint32_t* __restrict__ gst, uint32_t K,
+                                                        const G1Xyzz* __restrict__ pfirst,
+                                                        const G1Xyzz* __restrict__ plast,
+                                                        const uint32_t* __restrict__ heavy,
+                                                        const uint32_t* __restrict__ nheavy,
+                                                        G1Xyzz* __restrict__ bsum) {
+  __shared__ G1Xyzz sh[kBlock];
+  const uint32_t nh = *nheavy, tid = threadIdx.x;
+  for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {
+    const uint32_t g = heavy[h];
+    const uint32_t s = gst[g], e = gst[g + 1];
+    const uint32_t t0 = s / K, t1 = (e - 1) / K;
+    G1Xyzz acc = G1Xyzz::identity();
+    for (uint32_t t = t0 + 1 + tid; t <= t1; t += kBlock) acc = xyzz_add(acc, load_xyzz(pfirst, t));
+    sh[tid] = acc;
+    __syncthreads();
+    for (uint32_t st = kBlock / 2; st > 0; st >>= 1) {
+      if (tid < st) sh[tid] = xyzz_add(sh[tid], sh[tid + st]);
+      __syncthreads();
+    }
+    if (tid == 0) {
+      G1Xyzz head = (s == t0 * K) ? load_xyzz(pfirst, t0) : load_xyzz(plast, t0);
+      store_xyzz(bsum, g, xyzz_add(head, sh[0]));
+    }
+    __syncthreads();
+  }
 }
 
 // One bucket-reduction level over `groups` groups of N elements, segments of L = kRedL:
@@ -320,43 +359,34 @@ __global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, u
   if (tot_out) store_xyzz(tot_out, tid, run);
 }
 
-// Step 2 of the reduction.  Per window w (J segments, H = J/2), NG = 2 + log2(J) groups of H points:
-// q = 0, 1: the two halves of acc[w][*]; q = 2 + k: T[w][j] for the j with bit k set.  Each thread
-// sums F consecutive members of one group: out[(w*NG + q)*O + o].
-__global__ void __launch_bounds__(kBlock) k_subset_sum(const G1Xyzz* __restrict__ acc, const G1Xyzz* __restrict__ tot,
-                                                       uint32_t J, uint32_t logJ, uint32_t W, uint32_t F, uint32_t O,
-                                                       G1Xyzz* __restrict__ out) {
+// Step 2 fused: one 512-thread block per (window, group) sums the group's H members (strided,
+// ~H/512 serial adds per thread) and finishes with an LDS tree (9 levels) -> out[w*NG + q].
+static constexpr int kGroupBlock = 512;
+__global__ void __launch_bounds__(kGroupBlock) k_group_sum(const G1Xyzz* __restrict__ acc,
+                                                           const G1Xyzz* __restrict__ tot, uint32_t J,
+                                                           uint32_t logJ, G1Xyzz* __restrict__ out) {
+  __shared__ G1Xyzz sh[kGroupBlock];
   const uint32_t NG = 2 + logJ, H = J / 2;
-  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= W * NG * O) return;
-  uint32_t o = tid % O, q = (tid / O) % NG, w = tid / (O * NG);
-  uint32_t lo = o * F, hi = min(H, lo + F);
+  const uint32_t gid = blockIdx.x, w = gid / NG, q = gid % NG, tid = threadIdx.x;
   G1Xyzz s = G1Xyzz::identity();
-  for (uint32_t m = lo; m < hi; m++) {
+  for (uint32_t m = tid; m < H; m += kGroupBlock) {
     G1Xyzz x;
     if (q < 2) {
       x = load_xyzz(acc, w * J + q * H + m);
     } else {
-      uint32_t k = q - 2;
-      uint32_t j = ((m >> k) << (k + 1)) | (1u << k) | (m & ((1u << k) - 1));
+      const uint32_t k = q - 2;
+      const uint32_t j = ((m >> k) << (k + 1)) | (1u << k) | (m & ((1u << k) - 1));
       x = load_xyzz(tot, w * J + j);
     }
     s = xyzz_add(s, x);
   }
-  store_xyzz(out, tid, s);
-}
-
-// Plain sums: out[g][j] = sum of X[g][jF .. jF+F)
-__global__ void __launch_bounds__(kBlock) k_sum(const G1Xyzz* __restrict__ X, uint32_t N, uint32_t F, uint32_t J, uint32_t groups,
-                      G1Xyzz* __restrict__ out) {
-  uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= J * groups) return;
-  uint32_t g = tid / J, j = tid % J;
-  const G1Xyzz* x = X + (size_t)g * N;
-  uint32_t lo = j * F, hi = min(N, lo + F);
-  G1Xyzz acc = G1Xyzz::identity();
-  for (uint32_t i = lo; i < hi; i++) acc = xyzz_add(acc, load_xyzz(x, i));
-  store_xyzz(out, tid, acc);
+  sh[tid] = s;
+  __syncthreads();
+  for (uint32_t st = kGroupBlock / 2; st > 0; st >>= 1) {
+    if (tid < st) sh[tid] = xyzz_add(sh[tid], sh[tid + st]);
+    __syncthreads();
+  }
+  if (tid == 0) store_xyzz(out, gid, sh[0]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -376,6 +406,7 @@ MsmPlan msm_plan(size_t n) {
   int lg = 0;
   while ((size_t(1) << (lg + 1)) <= n) lg++;
   int c = lg - 4;
+  if (const char* e = getenv("SVGPU_WINDOW_BITS")) c = atoi(e);
   if (c < 4) c = 4;
   if (c > 16) c = 16;
   p.c = c;
@@ -386,6 +417,8 @@ MsmPlan msm_plan(size_t n) {
   uint64_t K = entries / (1u << 18);
   if (K < 4) K = 4;
   if (K > 32) K = 32;
+  if (const char* e = getenv("SVGPU_ACC_K")) K = (uint64_t)atoi(e);
+  if (K < 1) K = 1;
   p.K = (uint32_t)K;
   p.T = cdiv(entries, p.K);
   uint32_t want_ch = cdiv(256, p.W);
@@ -490,11 +523,10 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
   add(((size_t)p.T + 1) * 4);                 // tstart
   add((size_t)p.T * sizeof(G1Xyzz) * 2);      // pfirst, plast
   add((size_t)p.nbt * sizeof(G1Xyzz));        // bsum
-  const uint32_t kSubF = 4;
-  const uint32_t O1 = cdiv(p.J / 2, kSubF);   // outputs per group after the first subset launch
-  add((size_t)p.J * p.W * sizeof(G1Xyzz) * 2);         // acc_j, T_j
-  add((size_t)O1 * p.NG * p.W * sizeof(G1Xyzz) * 2);   // sum ping-pong
+  add((size_t)p.nbt * 4);                     // heavy-bucket queue
   const size_t nfinal = (size_t)p.W * p.NG;
+  add((size_t)p.J * p.W * sizeof(G1Xyzz) * 2);         // acc_j, T_j
+  add(nfinal * sizeof(G1Xyzz));                        // group sums
   SV_TRY(ws->reserve(bytes));
   SV_TRY(ws->reserve_pinned(nfinal * sizeof(G1Xyzz) + 256));
 
@@ -512,10 +544,11 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
   G1Xyzz* pfirst = ws->carve<G1Xyzz>(p.T);
   G1Xyzz* plast = ws->carve<G1Xyzz>(p.T);
   G1Xyzz* bsum = ws->carve<G1Xyzz>(p.nbt);
+  uint32_t* heavy = ws->carve<uint32_t>(p.nbt);
+  uint32_t* nheavy = err + 1;  // zeroed with the error flag
   G1Xyzz* racc = ws->carve<G1Xyzz>((size_t)p.J * p.W);
   G1Xyzz* rtot = ws->carve<G1Xyzz>((size_t)p.J * p.W);
-  G1Xyzz* ping = ws->carve<G1Xyzz>((size_t)O1 * p.NG * p.W);
-  G1Xyzz* pong = ws->carve<G1Xyzz>((size_t)O1 * p.NG * p.W);
+  G1Xyzz* ping = ws->carve<G1Xyzz>(nfinal);
 
   hipEvent_t* ev = ws->ev;
   SV_HIP(hipEventRecord(ev[0], st));
@@ -546,29 +579,15 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
   SV_HIP(hipGetLastError());
   SV_HIP(hipEventRecord(ev[3], st));
   hipLaunchKernelGGL(k_fixup, dim3(cdiv(p.nbt, kBlock)), dim3(kBlock), 0, st, gst, p.nbt, p.K, pfirst,
-                     plast, bsum);
+                     plast, bsum, heavy, nheavy);
+  hipLaunchKernelGGL(k_fixup_heavy, dim3(256), dim3(kBlock), 0, st, gst, p.K, pfirst, plast, heavy, nheavy,
+                     bsum);
   SV_HIP(hipEventRecord(ev[4], st));
   // bucket reduction: running sums over segments of kRedL buckets, then the subset sums
   hipLaunchKernelGGL(k_wsum, dim3(cdiv((uint64_t)p.J * p.W, kBlock)), dim3(kBlock), 0, st, bsum, p.B, p.J,
                      p.W, 1, racc, rtot);
-  hipLaunchKernelGGL(k_subset_sum, dim3(cdiv((uint64_t)O1 * p.NG * p.W, kBlock)), dim3(kBlock), 0, st, racc,
-                     rtot, p.J, p.logJ, p.W, kSubF, O1, ping);
+  hipLaunchKernelGGL(k_group_sum, dim3(p.NG * p.W), dim3(kGroupBlock), 0, st, racc, rtot, p.J, p.logJ, ping);
   const G1Xyzz* src = ping;
-  {
-    G1Xyzz* bufs[2] = {pong, ping};
-    int flip = 0;
-    uint32_t N = O1;
-    while (N > 1) {
-      uint32_t F = 4;
-      uint32_t J = cdiv(N, F);
-      G1Xyzz* dst = bufs[flip];
-      hipLaunchKernelGGL(k_sum, dim3(cdiv((uint64_t)J * p.NG * p.W, kBlock)), dim3(kBlock), 0, st, src, N, F, J,
-                         p.NG * p.W, dst);
-      src = dst;
-      flip ^= 1;
-      N = J;
-    }
-  }
   SV_HIP(hipGetLastError());
   SV_HIP(hipEventRecord(ev[5], st));
   SV_HIP(hipMemcpyAsync(ws->pinned, src, nfinal * sizeof(G1Xyzz), hipMemcpyDeviceToHost, st));

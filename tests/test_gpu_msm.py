@@ -138,3 +138,34 @@ def test_multi_device_host_api_consistent(gpu, oracle_cpp):
     exp = _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
     for g in (0, 1, 2):
         assert svgpu.msm_arrays(B, S, svgpu.SV_CANONICAL, num_gpus=g) == exp
+
+
+def test_adversarial_all_equal_scalars_2_18_is_fast(gpu, oracle_cpp):
+    """Every window's 2^18 entries land in ONE bucket: the heavy-bucket fixup path must keep this
+    both exact and fast (a serial join of 2^13 pieces per window took ~0.1 s before)."""
+    import time
+    import svgpu
+    from svgpu import device as dv
+    n = 1 << 18
+    B = oracle_cpp.gen_bases(b.SEED_BASES, n)
+    S = np.tile(np.array([0x0123456789ABCDEF, 0xFEDCBA9876543210, 0x1111111111111111, 0x0222222222222222],
+                         np.uint64), (n, 1))
+    Bd = torch.from_numpy(B.view(np.int64)).to(gpu)
+    Sd = torch.from_numpy(S.view(np.int64)).to(gpu)
+    got = dv.msm(Bd, Sd, svgpu.SV_CANONICAL)
+    t0 = time.perf_counter()
+    dv.msm(Bd, Sd, svgpu.SV_CANONICAL)
+    dt = time.perf_counter() - t0
+    assert got == _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
+    assert dt < 0.05, f"skewed-bucket MSM took {dt * 1e3:.1f} ms"
+
+
+@pytest.mark.parametrize("bits", [5, 9, 13, 14, 15])
+def test_window_bits_override(gpu, oracle_cpp, bits, monkeypatch):
+    """Every window size (incl. short top windows that concentrate digits) gives the same point."""
+    import svgpu
+    monkeypatch.setenv("SVGPU_WINDOW_BITS", str(bits))
+    n = 20000
+    B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=99)
+    S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=99)
+    assert svgpu.msm_arrays(B, S) == _to_pt(oracle_cpp.msm_pippenger(B, S, 0))

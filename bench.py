@@ -58,11 +58,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one process per GPU; SVGPU_DIST_BACKEND=gloo lets several ranks share one card (rehearsal)
+    backend = os.environ.get("SVGPU_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local_dev = local % ndev if backend == "gloo" else local
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
 
     import svgpu
     from svgpu import device as dv, parallel
@@ -97,7 +105,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     stats = dv.last_msm_stats()
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -120,7 +128,7 @@ def main():
         ff, _, _ = dv.decide(g2, sg2, L, R)
     torch.cuda.synchronize()
     barrier()
-    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     dec_s = float(dt.item())

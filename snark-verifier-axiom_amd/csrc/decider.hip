@@ -10,12 +10,14 @@
 // exponentiation, all in registers.  The coefficient reads are lane-uniform (scalar loads).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
 
 #include "curve.hpp"
 #include "decider.hpp"
+#include "fq12_lanes.hpp"
 #include "runtime.hpp"
 
 namespace sv {
@@ -47,6 +49,171 @@ __global__ void __launch_bounds__(64) k_decide(const G1Aff* __restrict__ lhs, co
   Fq12 e = final_exponentiation(f);
   verdict[i] = e.is_one() ? 1 : 0;
   if (gt) gt[i] = e;
+}
+
+// ---------------------------------------------------------------------------------------------
+// 6-lane groups: each accumulator is decided by a group of 8 lanes, lanes 0..5 holding the w^k
+// coefficients of the Fq12 accumulator (fq12_lanes.hpp); operands are exchanged through LDS.
+// Control flow is uniform across the wave (identity inputs use the neutral line 1), so the
+// single-wave block can use __syncthreads() between the write and read phases of each exchange.
+// ---------------------------------------------------------------------------------------------
+static constexpr int kGL = 8;                 // lanes per group (6 active)
+static constexpr int kGroups = 64 / kGL;      // groups per single-wave block
+__constant__ uint32_t c_gamma[3 * 6 * 16] = SV_GAMMA_TAB_INIT;
+__constant__ SqrTerm c_sqr[6][4] = SV_SQR_TERMS;
+__constant__ int8_t c_naf[ATE_NAF_LEN] = SV_ATE_NAF_INIT;
+
+struct Grp {
+  Fq2* a;
+  Fq2* b;
+  int k;
+  bool w;
+};
+
+__device__ __forceinline__ Fq2 g_mul(const Grp& G, const Fq2& x, const Fq2& y) {
+  if (G.w) {
+    G.a[G.k] = x;
+    G.b[G.k] = y;
+  }
+  __syncthreads();
+  Fq2 r = w_mul_lane(G.a, G.b, G.k);
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ Fq2 g_sqr(const Grp& G, const Fq2& x) {
+  if (G.w) G.a[G.k] = x;
+  __syncthreads();
+  Fq2 r = w_sqr_lane(G.a, G.k, c_sqr);
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ Fq2 g_line(const Grp& G, const Fq2& x, const Fq2& l0, const Fq2& l1, const Fq2& l3) {
+  if (G.w) G.a[G.k] = x;
+  __syncthreads();
+  Fq2 r = w_line_lane(G.a, l0, l1, l3, G.k);
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ Fq2 g_conj(const Grp& G, const Fq2& x) { return (G.k & 1) ? -x : x; }
+__device__ __forceinline__ Fq2 g_frob(const Grp& G, int n, const Fq2& x) {
+  Fq2 y = (n & 1) ? fq2_conj(x) : x;
+  if (G.k == 0) return y;
+  const uint32_t* t = c_gamma + ((n - 1) * 6 + G.k) * 16;
+  Fq2 c;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    c.c0.v[i] = t[i];
+    c.c1.v[i] = t[8 + i];
+  }
+  return y * c;
+}
+__device__ __noinline__ Fq2 g_inv(const Grp& G, const Fq2& x) {
+  if (G.w) G.a[G.k] = x;
+  __syncthreads();
+  Fq12 f;
+#pragma unroll
+  for (int k = 0; k < 6; k++) tower_coeff(f, k) = G.a[k];
+  __syncthreads();
+  Fq12 fi = fq12_inv(f);
+  return tower_coeff(fi, G.k);
+}
+__device__ __noinline__ Fq2 g_pow_x(const Grp& G, const Fq2& a) {
+  Fq2 r = a;
+  for (int b = 61; b >= 0; b--) {
+    r = g_sqr(G, r);
+    if ((BN_X >> b) & 1) r = g_mul(G, r, a);
+  }
+  return r;
+}
+__device__ __noinline__ Fq2 g_pow_small(const Grp& G, const Fq2& a, uint32_t e) {
+  Fq2 r = a;
+  int top = 31 - __builtin_clz(e);
+  for (int b = top - 1; b >= 0; b--) {
+    r = g_sqr(G, r);
+    if ((e >> b) & 1) r = g_mul(G, r, a);
+  }
+  return r;
+}
+
+// line coefficients for this step, evaluated at P (neutral line 1 when P is the identity)
+__device__ __forceinline__ void line_at(const LineCoeff* __restrict__ L, int idx, const G1Aff& p, bool use,
+                                        Fq2& l0, Fq2& l1, Fq2& l3) {
+  if (use) {
+    const LineCoeff c = L[idx];
+    l0 = c.c0 * p.y;
+    l1 = c.c3 * p.x;
+    l3 = c.c4;
+  } else {
+    l0 = Fq2::one();
+    l1 = Fq2::zero();
+    l3 = Fq2::zero();
+  }
+}
+
+__global__ void __launch_bounds__(64) k_decide6(const G1Aff* __restrict__ lhs, const G1Aff* __restrict__ rhs,
+                                                 uint32_t n, const LineCoeff* __restrict__ L1,
+                                                 const LineCoeff* __restrict__ L2, int mont_in,
+                                                 int32_t* __restrict__ verdict, Fq12* __restrict__ gt) {
+  __shared__ Fq2 sh[2 * kGroups * 6];
+  const int lane = threadIdx.x, grp = lane / kGL, kk = lane % kGL;
+  const uint32_t acc = blockIdx.x * kGroups + grp;
+  Grp G{sh + grp * 12, sh + grp * 12 + 6, kk < 6 ? kk : 5, kk < 6};
+  const bool valid = acc < n;
+  G1Aff p1 = {Fq::zero(), Fq::zero()}, p2 = p1;
+  if (valid) {
+    p1 = load_aff_d(lhs, acc, mont_in);
+    p2 = load_aff_d(rhs, acc, mont_in);
+  }
+  const bool use1 = !p1.is_identity(), use2 = !p2.is_identity();
+  Fq2 f = G.k == 0 ? Fq2::one() : Fq2::zero();
+  Fq2 l0, l1, l3;
+  int idx = 0;
+  for (int i = ATE_NAF_LEN - 1; i >= 1; i--) {
+    if (i != ATE_NAF_LEN - 1) f = g_sqr(G, f);
+    line_at(L1, idx, p1, use1, l0, l1, l3);
+    f = g_line(G, f, l0, l1, l3);
+    line_at(L2, idx, p2, use2, l0, l1, l3);
+    f = g_line(G, f, l0, l1, l3);
+    idx++;
+    if (c_naf[i - 1] != 0) {
+      line_at(L1, idx, p1, use1, l0, l1, l3);
+      f = g_line(G, f, l0, l1, l3);
+      line_at(L2, idx, p2, use2, l0, l1, l3);
+      f = g_line(G, f, l0, l1, l3);
+      idx++;
+    }
+  }
+  for (int s = 0; s < 2; s++) {
+    line_at(L1, idx, p1, use1, l0, l1, l3);
+    f = g_line(G, f, l0, l1, l3);
+    line_at(L2, idx, p2, use2, l0, l1, l3);
+    f = g_line(G, f, l0, l1, l3);
+    idx++;
+  }
+  // final exponentiation (same chain as curve.hpp final_exponentiation)
+  Fq2 fi = g_inv(G, f);
+  f = g_mul(G, g_conj(G, f), fi);
+  f = g_mul(G, g_frob(G, 2, f), f);
+  Fq2 fx = g_pow_x(G, f);
+  Fq2 fx2 = g_pow_x(G, fx);
+  Fq2 fx3 = g_pow_x(G, fx2);
+  Fq2 fx3_36 = g_pow_small(G, fx3, 36);
+  Fq2 l2v = g_mul(G, g_pow_small(G, fx2, 6), f);
+  Fq2 t = g_mul(G, g_mul(G, fx3_36, g_pow_small(G, fx2, 18)), g_pow_small(G, fx, 12));
+  Fq2 l1v = g_mul(G, g_conj(G, t), f);
+  t = g_mul(G, g_mul(G, g_mul(G, fx3_36, g_pow_small(G, fx2, 30)), g_pow_small(G, fx, 18)), g_sqr(G, f));
+  Fq2 l0v = g_conj(G, t);
+  Fq2 e = g_mul(G, g_mul(G, g_mul(G, l0v, g_frob(G, 1, l1v)), g_frob(G, 2, l2v)), g_frob(G, 3, f));
+  const bool one_k = G.k == 0 ? (e == Fq2::one()) : e.is_zero();
+  const uint64_t bal = __ballot(one_k || !G.w);
+  const bool ok = ((bal >> (grp * kGL)) & 0xFFull) == 0xFFull;
+  if (valid && G.w) {
+    if (G.k == 0) verdict[acc] = ok ? 1 : 0;
+    if (gt) {
+      Fq2* dst = reinterpret_cast<Fq2*>(gt + acc) + (G.k & 1) * 3 + (G.k >> 1);
+      *dst = e;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -137,10 +304,17 @@ int decide_run_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const vo
   int32_t* d_verdict = ws->carve<int32_t>(n);
   Fq12* d_gt = gt_host ? ws->carve<Fq12>(n) : nullptr;
   SV_HIP(hipEventRecord(ws->ev[0], st));
-  hipLaunchKernelGGL(k_decide, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st,
-                     reinterpret_cast<const G1Aff*>(d_lhs), reinterpret_cast<const G1Aff*>(d_rhs),
-                     (uint32_t)n, lines, lines + ATE_NUM_LINES, form == SV_MONTGOMERY ? 1 : 0,
-                     d_verdict, d_gt);
+  static const bool one_lane = getenv("SVGPU_DECIDER_1LANE") != nullptr;
+  if (one_lane)
+    hipLaunchKernelGGL(k_decide, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st,
+                       reinterpret_cast<const G1Aff*>(d_lhs), reinterpret_cast<const G1Aff*>(d_rhs),
+                       (uint32_t)n, lines, lines + ATE_NUM_LINES, form == SV_MONTGOMERY ? 1 : 0,
+                       d_verdict, d_gt);
+  else
+    hipLaunchKernelGGL(k_decide6, dim3((unsigned)((n + kGroups - 1) / kGroups)), dim3(64), 0, st,
+                       reinterpret_cast<const G1Aff*>(d_lhs), reinterpret_cast<const G1Aff*>(d_rhs),
+                       (uint32_t)n, lines, lines + ATE_NUM_LINES, form == SV_MONTGOMERY ? 1 : 0,
+                       d_verdict, d_gt);
   SV_HIP(hipGetLastError());
   SV_HIP(hipEventRecord(ws->ev[1], st));
   int32_t* hv = reinterpret_cast<int32_t*>(ws->pinned);

@@ -52,48 +52,108 @@ __global__ void __launch_bounds__(64) k_decide(const G1Aff* __restrict__ lhs, co
 }
 
 // ---------------------------------------------------------------------------------------------
-// 6-lane groups: each accumulator is decided by a group of 8 lanes, lanes 0..5 holding the w^k
-// coefficients of the Fq12 accumulator (fq12_lanes.hpp); operands are exchanged through LDS.
-// Control flow is uniform across the wave (identity inputs use the neutral line 1), so the
-// single-wave block can use __syncthreads() between the write and read phases of each exchange.
+// Lane groups: each accumulator is decided by 6 x S lanes.  Lane (k, s) holds the w^k coefficient
+// g_k of the Fq12 accumulator (replicated over its S sub-lanes; fq12_lanes.hpp), and computes the
+// products of its coefficient whose index is = s (mod S); the S partial sums are combined with
+// cross-lane xor-shuffles, so an Fq12 multiply costs ceil(6/S) Fq2 products of latency, a square
+// ceil(4/S), a sparse line step ceil(3/S).  Operands are exchanged through LDS.  Control flow is
+// uniform across the wave (identity inputs use the neutral line 1), so the single-wave block can
+// use __syncthreads() between the write and read phases of each exchange.
 // ---------------------------------------------------------------------------------------------
-static constexpr int kGL = 8;                 // lanes per group (6 active)
-static constexpr int kGroups = 64 / kGL;      // groups per single-wave block
 __constant__ uint32_t c_gamma[3 * 6 * 16] = SV_GAMMA_TAB_INIT;
 __constant__ SqrTerm c_sqr[6][4] = SV_SQR_TERMS;
 __constant__ int8_t c_naf[ATE_NAF_LEN] = SV_ATE_NAF_INIT;
 
 struct Grp {
-  Fq2* a;
-  Fq2* b;
-  int k;
-  bool w;
+  Fq2* a;  // this group's 6 LDS slots for operand A
+  Fq2* b;  // ... and operand B
+  int k;   // coefficient index (lanes past 6*S mirror k = 5 and never write)
+  int s;   // sub-lane
+  bool w;  // writer (s == 0, active)
 };
 
+template <int S>
+__device__ __forceinline__ Fq2 sub_reduce(Fq2 v) {
+  // sum over the S consecutive sub-lanes of one coefficient (S = 1, 2, 4)
+#pragma unroll
+  for (int m = 1; m < S; m <<= 1) {
+    Fq2 o;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      o.c0.v[i] = __shfl_xor(v.c0.v[i], m);
+      o.c1.v[i] = __shfl_xor(v.c1.v[i], m);
+    }
+    v = v + o;
+  }
+  return v;
+}
+
+template <int S>
 __device__ __forceinline__ Fq2 g_mul(const Grp& G, const Fq2& x, const Fq2& y) {
   if (G.w) {
     G.a[G.k] = x;
     G.b[G.k] = y;
   }
   __syncthreads();
-  Fq2 r = w_mul_lane(G.a, G.b, G.k);
+  Fq2 lo = Fq2::zero(), hi = Fq2::zero();
+#pragma unroll
+  for (int t = 0; t < (6 + S - 1) / S; t++) {
+    const int i = t * S + G.s;
+    if (i < 6) {
+      const int j = G.k - i;
+      const Fq2 p = G.a[i] * G.b[j < 0 ? j + 6 : j];
+      if (j >= 0) lo = lo + p;
+      else hi = hi + p;
+    }
+  }
   __syncthreads();
-  return r;
+  return sub_reduce<S>(lo + fq2_mul_xi(hi));
 }
+
+template <int S>
 __device__ __forceinline__ Fq2 g_sqr(const Grp& G, const Fq2& x) {
   if (G.w) G.a[G.k] = x;
   __syncthreads();
-  Fq2 r = w_sqr_lane(G.a, G.k, c_sqr);
+  Fq2 lo = Fq2::zero(), hi = Fq2::zero();
+#pragma unroll
+  for (int t = 0; t < (4 + S - 1) / S; t++) {
+    const int slot = t * S + G.s;
+    if (slot < 4) {
+      const SqrTerm q = c_sqr[G.k][slot];
+      if (q.i >= 0) {
+        Fq2 p = G.a[q.i] * G.a[q.j];
+        if (q.dbl) p = p + p;
+        if (q.xi) hi = hi + p;
+        else lo = lo + p;
+      }
+    }
+  }
   __syncthreads();
-  return r;
+  return sub_reduce<S>(lo + fq2_mul_xi(hi));
 }
+
+// f * (l0 + l1 w + l3 w^3)
+template <int S>
 __device__ __forceinline__ Fq2 g_line(const Grp& G, const Fq2& x, const Fq2& l0, const Fq2& l1, const Fq2& l3) {
   if (G.w) G.a[G.k] = x;
   __syncthreads();
-  Fq2 r = w_line_lane(G.a, l0, l1, l3, G.k);
+  Fq2 lo = Fq2::zero(), hi = Fq2::zero();
+#pragma unroll
+  for (int t = 0; t < (3 + S - 1) / S; t++) {
+    const int term = t * S + G.s;
+    if (term < 3) {
+      const int sh = term == 0 ? 0 : (term == 1 ? 1 : 3);
+      const int src = G.k - sh;
+      const Fq2& l = term == 0 ? l0 : (term == 1 ? l1 : l3);
+      const Fq2 p = G.a[src < 0 ? src + 6 : src] * l;
+      if (src >= 0) lo = lo + p;
+      else hi = hi + p;
+    }
+  }
   __syncthreads();
-  return r;
+  return sub_reduce<S>(lo + fq2_mul_xi(hi));
 }
+
 __device__ __forceinline__ Fq2 g_conj(const Grp& G, const Fq2& x) { return (G.k & 1) ? -x : x; }
 __device__ __forceinline__ Fq2 g_frob(const Grp& G, int n, const Fq2& x) {
   Fq2 y = (n & 1) ? fq2_conj(x) : x;
@@ -117,20 +177,22 @@ __device__ __noinline__ Fq2 g_inv(const Grp& G, const Fq2& x) {
   Fq12 fi = fq12_inv(f);
   return tower_coeff(fi, G.k);
 }
+template <int S>
 __device__ __noinline__ Fq2 g_pow_x(const Grp& G, const Fq2& a) {
   Fq2 r = a;
   for (int b = 61; b >= 0; b--) {
-    r = g_sqr(G, r);
-    if ((BN_X >> b) & 1) r = g_mul(G, r, a);
+    r = g_sqr<S>(G, r);
+    if ((BN_X >> b) & 1) r = g_mul<S>(G, r, a);
   }
   return r;
 }
+template <int S>
 __device__ __noinline__ Fq2 g_pow_small(const Grp& G, const Fq2& a, uint32_t e) {
   Fq2 r = a;
-  int top = 31 - __builtin_clz(e);
+  const int top = 31 - __builtin_clz(e);
   for (int b = top - 1; b >= 0; b--) {
-    r = g_sqr(G, r);
-    if ((e >> b) & 1) r = g_mul(G, r, a);
+    r = g_sqr<S>(G, r);
+    if ((e >> b) & 1) r = g_mul<S>(G, r, a);
   }
   return r;
 }
@@ -150,14 +212,19 @@ __device__ __forceinline__ void line_at(const LineCoeff* __restrict__ L, int idx
   }
 }
 
-__global__ void __launch_bounds__(64) k_decide6(const G1Aff* __restrict__ lhs, const G1Aff* __restrict__ rhs,
-                                                 uint32_t n, const LineCoeff* __restrict__ L1,
-                                                 const LineCoeff* __restrict__ L2, int mont_in,
-                                                 int32_t* __restrict__ verdict, Fq12* __restrict__ gt) {
-  __shared__ Fq2 sh[2 * kGroups * 6];
-  const int lane = threadIdx.x, grp = lane / kGL, kk = lane % kGL;
-  const uint32_t acc = blockIdx.x * kGroups + grp;
-  Grp G{sh + grp * 12, sh + grp * 12 + 6, kk < 6 ? kk : 5, kk < 6};
+template <int S>
+__global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ lhs, const G1Aff* __restrict__ rhs,
+                                                      uint32_t n, const LineCoeff* __restrict__ L1,
+                                                      const LineCoeff* __restrict__ L2, int mont_in,
+                                                      int32_t* __restrict__ verdict, Fq12* __restrict__ gt) {
+  constexpr int GL = 8 * S;         // lanes per group (6 * S active)
+  constexpr int NGRP = 64 / GL;     // groups per single-wave block
+  __shared__ Fq2 sh[2 * NGRP * 6];
+  const int lane = threadIdx.x, grp = lane / GL, gl = lane % GL;
+  const bool active = gl < 6 * S;
+  const int k = active ? gl / S : 5, sub = active ? gl % S : 0;
+  const uint32_t acc = blockIdx.x * NGRP + grp;
+  Grp G{sh + grp * 12, sh + grp * 12 + 6, k, sub, active && sub == 0};
   const bool valid = acc < n;
   G1Aff p1 = {Fq::zero(), Fq::zero()}, p2 = p1;
   if (valid) {
@@ -169,44 +236,46 @@ __global__ void __launch_bounds__(64) k_decide6(const G1Aff* __restrict__ lhs, c
   Fq2 l0, l1, l3;
   int idx = 0;
   for (int i = ATE_NAF_LEN - 1; i >= 1; i--) {
-    if (i != ATE_NAF_LEN - 1) f = g_sqr(G, f);
+    if (i != ATE_NAF_LEN - 1) f = g_sqr<S>(G, f);
     line_at(L1, idx, p1, use1, l0, l1, l3);
-    f = g_line(G, f, l0, l1, l3);
+    f = g_line<S>(G, f, l0, l1, l3);
     line_at(L2, idx, p2, use2, l0, l1, l3);
-    f = g_line(G, f, l0, l1, l3);
+    f = g_line<S>(G, f, l0, l1, l3);
     idx++;
     if (c_naf[i - 1] != 0) {
       line_at(L1, idx, p1, use1, l0, l1, l3);
-      f = g_line(G, f, l0, l1, l3);
+      f = g_line<S>(G, f, l0, l1, l3);
       line_at(L2, idx, p2, use2, l0, l1, l3);
-      f = g_line(G, f, l0, l1, l3);
+      f = g_line<S>(G, f, l0, l1, l3);
       idx++;
     }
   }
-  for (int s = 0; s < 2; s++) {
+  for (int st = 0; st < 2; st++) {
     line_at(L1, idx, p1, use1, l0, l1, l3);
-    f = g_line(G, f, l0, l1, l3);
+    f = g_line<S>(G, f, l0, l1, l3);
     line_at(L2, idx, p2, use2, l0, l1, l3);
-    f = g_line(G, f, l0, l1, l3);
+    f = g_line<S>(G, f, l0, l1, l3);
     idx++;
   }
   // final exponentiation (same chain as curve.hpp final_exponentiation)
   Fq2 fi = g_inv(G, f);
-  f = g_mul(G, g_conj(G, f), fi);
-  f = g_mul(G, g_frob(G, 2, f), f);
-  Fq2 fx = g_pow_x(G, f);
-  Fq2 fx2 = g_pow_x(G, fx);
-  Fq2 fx3 = g_pow_x(G, fx2);
-  Fq2 fx3_36 = g_pow_small(G, fx3, 36);
-  Fq2 l2v = g_mul(G, g_pow_small(G, fx2, 6), f);
-  Fq2 t = g_mul(G, g_mul(G, fx3_36, g_pow_small(G, fx2, 18)), g_pow_small(G, fx, 12));
-  Fq2 l1v = g_mul(G, g_conj(G, t), f);
-  t = g_mul(G, g_mul(G, g_mul(G, fx3_36, g_pow_small(G, fx2, 30)), g_pow_small(G, fx, 18)), g_sqr(G, f));
+  f = g_mul<S>(G, g_conj(G, f), fi);
+  f = g_mul<S>(G, g_frob(G, 2, f), f);
+  Fq2 fx = g_pow_x<S>(G, f);
+  Fq2 fx2 = g_pow_x<S>(G, fx);
+  Fq2 fx3 = g_pow_x<S>(G, fx2);
+  Fq2 fx3_36 = g_pow_small<S>(G, fx3, 36);
+  Fq2 l2v = g_mul<S>(G, g_pow_small<S>(G, fx2, 6), f);
+  Fq2 t = g_mul<S>(G, g_mul<S>(G, fx3_36, g_pow_small<S>(G, fx2, 18)), g_pow_small<S>(G, fx, 12));
+  Fq2 l1v = g_mul<S>(G, g_conj(G, t), f);
+  t = g_mul<S>(G, g_mul<S>(G, g_mul<S>(G, fx3_36, g_pow_small<S>(G, fx2, 30)), g_pow_small<S>(G, fx, 18)),
+               g_sqr<S>(G, f));
   Fq2 l0v = g_conj(G, t);
-  Fq2 e = g_mul(G, g_mul(G, g_mul(G, l0v, g_frob(G, 1, l1v)), g_frob(G, 2, l2v)), g_frob(G, 3, f));
+  Fq2 e = g_mul<S>(G, g_mul<S>(G, g_mul<S>(G, l0v, g_frob(G, 1, l1v)), g_frob(G, 2, l2v)), g_frob(G, 3, f));
   const bool one_k = G.k == 0 ? (e == Fq2::one()) : e.is_zero();
-  const uint64_t bal = __ballot(one_k || !G.w);
-  const bool ok = ((bal >> (grp * kGL)) & 0xFFull) == 0xFFull;
+  const uint64_t bal = __ballot(one_k || !active);
+  const uint64_t gmask = GL == 64 ? ~0ull : ((1ull << GL) - 1);
+  const bool ok = ((bal >> (grp * GL)) & gmask) == gmask;
   if (valid && G.w) {
     if (G.k == 0) verdict[acc] = ok ? 1 : 0;
     if (gt) {
@@ -304,17 +373,24 @@ int decide_run_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const vo
   int32_t* d_verdict = ws->carve<int32_t>(n);
   Fq12* d_gt = gt_host ? ws->carve<Fq12>(n) : nullptr;
   SV_HIP(hipEventRecord(ws->ev[0], st));
-  static const bool one_lane = getenv("SVGPU_DECIDER_1LANE") != nullptr;
-  if (one_lane)
-    hipLaunchKernelGGL(k_decide, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st,
-                       reinterpret_cast<const G1Aff*>(d_lhs), reinterpret_cast<const G1Aff*>(d_rhs),
-                       (uint32_t)n, lines, lines + ATE_NUM_LINES, form == SV_MONTGOMERY ? 1 : 0,
-                       d_verdict, d_gt);
+  // SVGPU_DECIDER_LANES = 1 (one lane per accumulator, tower arithmetic), 6, 12 or 24 (6 x S lanes)
+  static const int lanes = getenv("SVGPU_DECIDER_LANES") ? atoi(getenv("SVGPU_DECIDER_LANES")) : 24;
+  const G1Aff* dl = reinterpret_cast<const G1Aff*>(d_lhs);
+  const G1Aff* dr = reinterpret_cast<const G1Aff*>(d_rhs);
+  const int mont = form == SV_MONTGOMERY ? 1 : 0;
+  const LineCoeff* L2 = lines + ATE_NUM_LINES;
+  if (lanes == 1)
+    hipLaunchKernelGGL(k_decide, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, dl, dr, (uint32_t)n, lines, L2,
+                       mont, d_verdict, d_gt);
+  else if (lanes == 6)
+    hipLaunchKernelGGL(k_decide_lanes<1>, dim3((unsigned)((n + 7) / 8)), dim3(64), 0, st, dl, dr, (uint32_t)n,
+                       lines, L2, mont, d_verdict, d_gt);
+  else if (lanes == 12)
+    hipLaunchKernelGGL(k_decide_lanes<2>, dim3((unsigned)((n + 3) / 4)), dim3(64), 0, st, dl, dr, (uint32_t)n,
+                       lines, L2, mont, d_verdict, d_gt);
   else
-    hipLaunchKernelGGL(k_decide6, dim3((unsigned)((n + kGroups - 1) / kGroups)), dim3(64), 0, st,
-                       reinterpret_cast<const G1Aff*>(d_lhs), reinterpret_cast<const G1Aff*>(d_rhs),
-                       (uint32_t)n, lines, lines + ATE_NUM_LINES, form == SV_MONTGOMERY ? 1 : 0,
-                       d_verdict, d_gt);
+    hipLaunchKernelGGL(k_decide_lanes<4>, dim3((unsigned)((n + 1) / 2)), dim3(64), 0, st, dl, dr, (uint32_t)n,
+                       lines, L2, mont, d_verdict, d_gt);
   SV_HIP(hipGetLastError());
   SV_HIP(hipEventRecord(ws->ev[1], st));
   int32_t* hv = reinterpret_cast<int32_t*>(ws->pinned);

@@ -94,6 +94,35 @@ SV_HD Fe<M> fe_select(bool c, const Fe<M>& a, const Fe<M>& b) {
   return r;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// Device add/sub as explicit carry chains (__builtin_addc/subc -> v_addc/v_subb through VCC, hazard
+// padding by the compiler): 32 VALU per op instead of ~90 for the 64-bit-intermediate C form.
+template <class M>
+SV_HD Fe<M> operator+(const Fe<M>& a, const Fe<M>& b) {
+  Fe<M> t, d, r;
+  uint32_t c = 0, br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) t.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+  // a + b < 2p < 2^255: no carry out; subtract p when t >= p
+#pragma unroll
+  for (int i = 0; i < 8; i++) d.v[i] = __builtin_subc(t.v[i], M::p(i), br, &br);
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = br ? t.v[i] : d.v[i];
+  return r;
+}
+
+template <class M>
+SV_HD Fe<M> operator-(const Fe<M>& a, const Fe<M>& b) {
+  Fe<M> t, r;
+  uint32_t c = 0, br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) t.v[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
+  const uint32_t mask = 0u - br;  // add p back on borrow
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = __builtin_addc(t.v[i], M::p(i) & mask, c, &c);
+  return r;
+}
+#else
 template <class M>
 SV_HD Fe<M> operator+(const Fe<M>& a, const Fe<M>& b) {
   uint32_t t[8];
@@ -141,6 +170,8 @@ SV_HD Fe<M> operator-(const Fe<M>& a, const Fe<M>& b) {
   return r;
 }
 
+#endif
+
 template <class M>
 SV_HD Fe<M> operator-(const Fe<M>& a) {
   return Fe<M>::zero() - a;
@@ -155,12 +186,27 @@ SV_HD Fe<M> fe_dbl(const Fe<M>& a) {
 // acc (64 bit) += a * b with the carry out of v_mad_u64_u32 collected in ovf: two VALU
 // instructions per partial product and no re-packing of 64-bit addends (the compiler's CIOS
 // lowering spends ~2.3 v_mov per product on that; tools/ubench_mulvar: 99.6 -> 130 G mul/s).
+// VCC hazard: the v_addc reads VCC right after the quarter-rate v_mad_u64_u32 wrote it; the mad's
+// multi-pass issue occupies the wave's VALU past the 2-state VALU-SGPR-write window, so no s_nop is
+// needed inside a block (every result is checked bit-exact against the oracle in tests/).  hipcc
+// pads one state after each asm block, so products are issued four per block (single-wave latency
+// 737 -> 607 ns per multiply, tools/ubench_mulgroup).
+#define SV_MAC_STEP(A, B) "v_mad_u64_u32 %0, vcc, " A ", " B ", %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
 __device__ __forceinline__ void mac_carry(uint64_t& acc, uint32_t& ovf, uint32_t a, uint32_t b) {
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+  asm(SV_MAC_STEP("%2", "%3") : "+v"(acc), "+v"(ovf) : "v"(a), "v"(b) : "vcc");
+}
+__device__ __forceinline__ void mac_carry2(uint64_t& acc, uint32_t& ovf, uint32_t a0, uint32_t b0, uint32_t a1,
+                                           uint32_t b1) {
+  asm(SV_MAC_STEP("%2", "%3") SV_MAC_STEP("%4", "%5")
+      : "+v"(acc), "+v"(ovf) : "v"(a0), "v"(b0), "v"(a1), "v"(b1) : "vcc");
+}
+__device__ __forceinline__ void mac_carry4(uint64_t& acc, uint32_t& ovf, const uint32_t* x, const uint32_t* y) {
+  asm(SV_MAC_STEP("%2", "%3") SV_MAC_STEP("%4", "%5") SV_MAC_STEP("%6", "%7") SV_MAC_STEP("%8", "%9")
       : "+v"(acc), "+v"(ovf)
-      : "v"(a), "v"(b)
+      : "v"(x[0]), "v"(y[0]), "v"(x[1]), "v"(y[1]), "v"(x[2]), "v"(y[2]), "v"(x[3]), "v"(y[3])
       : "vcc");
 }
+#undef SV_MAC_STEP
 
 // Montgomery multiplication by finely integrated product scanning: column k accumulates
 // a_i b_{k-i} and m_i p_{k-i} in (acc, ovf); for k < 8 the column's low word fixes m_k.
@@ -171,16 +217,34 @@ SV_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
   uint32_t ovf = 0;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
+    // the column's products (a_i b_{k-i}, then m_i p_{k-i}); counts are compile-time constants
+    uint32_t xs[16], ys[16];
+    int c = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int j = k - i;
-      if (j >= 0 && j < 8) mac_carry(acc, ovf, a.v[i], b.v[j]);
+      if (j >= 0 && j < 8) {
+        xs[c] = a.v[i];
+        ys[c] = b.v[j];
+        c++;
+      }
     }
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int j = k - i;
-      if (i < k && j >= 1 && j < 8) mac_carry(acc, ovf, m[i], M::p(j));
+      if (i < k && j >= 1 && j < 8) {
+        xs[c] = m[i];
+        ys[c] = M::p(j);
+        c++;
+      }
     }
+    int q = 0;
+#pragma unroll
+    for (; q + 3 < c; q += 4) mac_carry4(acc, ovf, xs + q, ys + q);
+#pragma unroll
+    for (; q + 1 < c; q += 2) mac_carry2(acc, ovf, xs[q], ys[q], xs[q + 1], ys[q + 1]);
+#pragma unroll
+    for (; q < c; q++) mac_carry(acc, ovf, xs[q], ys[q]);
     if (k < 8) {
       m[k] = (uint32_t)acc * M::NP0;
       mac_carry(acc, ovf, m[k], M::p(0));

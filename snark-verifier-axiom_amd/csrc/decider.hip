@@ -5,9 +5,9 @@
 //
 // The two G2 points are fixed per call, so their Miller-loop line coefficients (88 steps x 3 Fq2
 // each, 33.8 KB for both) are computed once on the host (G2Prepared::from, which the reference
-// redoes inside every decide, decider.rs:64) and uploaded; every accumulator is then one lane:
-// a 2-term multi-Miller loop with sparse 034 line multiplications and the exact final
-// exponentiation, all in registers.  The coefficient reads are lane-uniform (scalar loads).
+// redoes inside every decide, decider.rs:64) and uploaded.  Each accumulator is then decided by a
+// group of 6 x S lanes (below): a 2-term multi-Miller loop with sparse 034 line multiplications and
+// the exact final exponentiation (the chain of curve.hpp), Fq12 spread one coefficient per 6 lanes.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -37,20 +37,6 @@ __device__ __forceinline__ G1Aff load_aff_d(const G1Aff* __restrict__ a, uint32_
   return r;
 }
 
-__global__ void __launch_bounds__(64) k_decide(const G1Aff* __restrict__ lhs, const G1Aff* __restrict__ rhs,
-                                                uint32_t n, const LineCoeff* __restrict__ L1,
-                                                const LineCoeff* __restrict__ L2, int mont_in,
-                                                int32_t* __restrict__ verdict, Fq12* __restrict__ gt) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  G1Aff p1 = load_aff_d(lhs, i, mont_in);
-  G1Aff p2 = load_aff_d(rhs, i, mont_in);
-  Fq12 f = miller_loop_2(p1, L1, p2, L2);
-  Fq12 e = final_exponentiation(f);
-  verdict[i] = e.is_one() ? 1 : 0;
-  if (gt) gt[i] = e;
-}
-
 // ---------------------------------------------------------------------------------------------
 // Lane groups: each accumulator is decided by 6 x S lanes.  Lane (k, s) holds the w^k coefficient
 // g_k of the Fq12 accumulator (replicated over its S sub-lanes; fq12_lanes.hpp), and computes the
@@ -65,11 +51,12 @@ __constant__ SqrTerm c_sqr[6][4] = SV_SQR_TERMS;
 __constant__ int8_t c_naf[ATE_NAF_LEN] = SV_ATE_NAF_INIT;
 
 struct Grp {
-  Fq2* a;  // this group's 6 LDS slots for operand A
-  Fq2* b;  // ... and operand B
-  int k;   // coefficient index (lanes past 6*S mirror k = 5 and never write)
-  int s;   // sub-lane
-  bool w;  // writer (s == 0, active)
+  Fq2* a;         // this group's 6 LDS slots for operand A
+  Fq2* b;         // ... and operand B
+  int k;          // coefficient index (lanes past 6*S mirror k = 5 and never write)
+  int s;          // sub-lane
+  bool w;         // writer (s == 0, active)
+  SqrTerm sq[4];  // this lane's square terms (slots s, s + S, ...), kept in registers
 };
 
 template <int S>
@@ -119,7 +106,7 @@ __device__ __forceinline__ Fq2 g_sqr(const Grp& G, const Fq2& x) {
   for (int t = 0; t < (4 + S - 1) / S; t++) {
     const int slot = t * S + G.s;
     if (slot < 4) {
-      const SqrTerm q = c_sqr[G.k][slot];
+      const SqrTerm q = G.sq[t];
       if (q.i >= 0) {
         Fq2 p = G.a[q.i] * G.a[q.j];
         if (q.dbl) p = p + p;
@@ -197,18 +184,28 @@ __device__ __noinline__ Fq2 g_pow_small(const Grp& G, const Fq2& a, uint32_t e) 
   return r;
 }
 
-// line coefficients for this step, evaluated at P (neutral line 1 when P is the identity)
-__device__ __forceinline__ void line_at(const LineCoeff* __restrict__ L, int idx, const G1Aff& p, bool use,
-                                        Fq2& l0, Fq2& l1, Fq2& l3) {
-  if (use) {
-    const LineCoeff c = L[idx];
-    l0 = c.c0 * p.y;
-    l1 = c.c3 * p.x;
-    l3 = c.c4;
-  } else {
-    l0 = Fq2::one();
-    l1 = Fq2::zero();
-    l3 = Fq2::zero();
+// Prologue: the group's lanes evaluate all 2 x ATE_NUM_LINES lines at their accumulator's points
+// into LDS (l0 = c0 yP, l1 = c3 xP, l3 = c4; the neutral line 1 when P is the identity), so the
+// Miller loop's line steps do no global loads and no line arithmetic on the critical path.
+__device__ __forceinline__ void eval_lines(LineCoeff* __restrict__ E, const LineCoeff* __restrict__ L1,
+                                           const LineCoeff* __restrict__ L2, const G1Aff& p1, const G1Aff& p2,
+                                           int lane_in_group, int group_lanes) {
+  for (int it = lane_in_group; it < 2 * ATE_NUM_LINES; it += group_lanes) {
+    const int idx = it >> 1;
+    const bool second = it & 1;
+    const G1Aff& p = second ? p2 : p1;
+    LineCoeff out;
+    if (!p.is_identity()) {
+      const LineCoeff c = (second ? L2 : L1)[idx];
+      out.c0 = c.c0 * p.y;
+      out.c3 = c.c3 * p.x;
+      out.c4 = c.c4;
+    } else {
+      out.c0 = Fq2::one();
+      out.c3 = Fq2::zero();
+      out.c4 = Fq2::zero();
+    }
+    E[it] = out;
   }
 }
 
@@ -216,48 +213,53 @@ template <int S>
 __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ lhs, const G1Aff* __restrict__ rhs,
                                                       uint32_t n, const LineCoeff* __restrict__ L1,
                                                       const LineCoeff* __restrict__ L2, int mont_in,
-                                                      int32_t* __restrict__ verdict, Fq12* __restrict__ gt) {
+                                                      int32_t* __restrict__ verdict, Fq12* __restrict__ gt,
+                                                      int phases) {
   constexpr int GL = 8 * S;         // lanes per group (6 * S active)
   constexpr int NGRP = 64 / GL;     // groups per single-wave block
   __shared__ Fq2 sh[2 * NGRP * 6];
+  __shared__ LineCoeff ev[NGRP][2 * ATE_NUM_LINES];
   const int lane = threadIdx.x, grp = lane / GL, gl = lane % GL;
   const bool active = gl < 6 * S;
   const int k = active ? gl / S : 5, sub = active ? gl % S : 0;
   const uint32_t acc = blockIdx.x * NGRP + grp;
-  Grp G{sh + grp * 12, sh + grp * 12 + 6, k, sub, active && sub == 0};
+  Grp G{sh + grp * 12, sh + grp * 12 + 6, k, sub, active && sub == 0, {}};
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    const int slot = t * S + sub;
+    G.sq[t] = slot < 4 ? c_sqr[k][slot] : SqrTerm{-1, -1, 0, 0};
+  }
   const bool valid = acc < n;
   G1Aff p1 = {Fq::zero(), Fq::zero()}, p2 = p1;
   if (valid) {
     p1 = load_aff_d(lhs, acc, mont_in);
     p2 = load_aff_d(rhs, acc, mont_in);
   }
-  const bool use1 = !p1.is_identity(), use2 = !p2.is_identity();
+  eval_lines(ev[grp], L1, L2, p1, p2, gl, GL);
+  __syncthreads();
+  const LineCoeff* E = ev[grp];
   Fq2 f = G.k == 0 ? Fq2::one() : Fq2::zero();
-  Fq2 l0, l1, l3;
   int idx = 0;
-  for (int i = ATE_NAF_LEN - 1; i >= 1; i--) {
+  for (int i = ATE_NAF_LEN - 1; i >= 1 && (phases & 1); i--) {
     if (i != ATE_NAF_LEN - 1) f = g_sqr<S>(G, f);
-    line_at(L1, idx, p1, use1, l0, l1, l3);
-    f = g_line<S>(G, f, l0, l1, l3);
-    line_at(L2, idx, p2, use2, l0, l1, l3);
-    f = g_line<S>(G, f, l0, l1, l3);
+    f = g_line<S>(G, f, E[2 * idx].c0, E[2 * idx].c3, E[2 * idx].c4);
+    f = g_line<S>(G, f, E[2 * idx + 1].c0, E[2 * idx + 1].c3, E[2 * idx + 1].c4);
     idx++;
     if (c_naf[i - 1] != 0) {
-      line_at(L1, idx, p1, use1, l0, l1, l3);
-      f = g_line<S>(G, f, l0, l1, l3);
-      line_at(L2, idx, p2, use2, l0, l1, l3);
-      f = g_line<S>(G, f, l0, l1, l3);
+      f = g_line<S>(G, f, E[2 * idx].c0, E[2 * idx].c3, E[2 * idx].c4);
+      f = g_line<S>(G, f, E[2 * idx + 1].c0, E[2 * idx + 1].c3, E[2 * idx + 1].c4);
       idx++;
     }
   }
-  for (int st = 0; st < 2; st++) {
-    line_at(L1, idx, p1, use1, l0, l1, l3);
-    f = g_line<S>(G, f, l0, l1, l3);
-    line_at(L2, idx, p2, use2, l0, l1, l3);
-    f = g_line<S>(G, f, l0, l1, l3);
+  for (int st = 0; st < 2 && (phases & 1); st++) {
+    f = g_line<S>(G, f, E[2 * idx].c0, E[2 * idx].c3, E[2 * idx].c4);
+    f = g_line<S>(G, f, E[2 * idx + 1].c0, E[2 * idx + 1].c3, E[2 * idx + 1].c4);
     idx++;
   }
   // final exponentiation (same chain as curve.hpp final_exponentiation)
+  // (phases: debug/profiling knob SVGPU_DECIDER_PHASES, 3 = both halves; results are only valid at 3)
+  Fq2 e = f;
+  if (phases & 2) {
   Fq2 fi = g_inv(G, f);
   f = g_mul<S>(G, g_conj(G, f), fi);
   f = g_mul<S>(G, g_frob(G, 2, f), f);
@@ -271,7 +273,8 @@ __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ l
   t = g_mul<S>(G, g_mul<S>(G, g_mul<S>(G, fx3_36, g_pow_small<S>(G, fx2, 30)), g_pow_small<S>(G, fx, 18)),
                g_sqr<S>(G, f));
   Fq2 l0v = g_conj(G, t);
-  Fq2 e = g_mul<S>(G, g_mul<S>(G, g_mul<S>(G, l0v, g_frob(G, 1, l1v)), g_frob(G, 2, l2v)), g_frob(G, 3, f));
+  e = g_mul<S>(G, g_mul<S>(G, g_mul<S>(G, l0v, g_frob(G, 1, l1v)), g_frob(G, 2, l2v)), g_frob(G, 3, f));
+  }
   const bool one_k = G.k == 0 ? (e == Fq2::one()) : e.is_zero();
   const uint64_t bal = __ballot(one_k || !active);
   const uint64_t gmask = GL == 64 ? ~0ull : ((1ull << GL) - 1);
@@ -373,24 +376,19 @@ int decide_run_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const vo
   int32_t* d_verdict = ws->carve<int32_t>(n);
   Fq12* d_gt = gt_host ? ws->carve<Fq12>(n) : nullptr;
   SV_HIP(hipEventRecord(ws->ev[0], st));
-  // SVGPU_DECIDER_LANES = 1 (one lane per accumulator, tower arithmetic), 6, 12 or 24 (6 x S lanes)
-  static const int lanes = getenv("SVGPU_DECIDER_LANES") ? atoi(getenv("SVGPU_DECIDER_LANES")) : 24;
+  // SVGPU_DECIDER_LANES = 48 (6 x 8 lanes per accumulator, 1 per wave; default) or 24 (6 x 4, 2 per wave)
+  static const int lanes = getenv("SVGPU_DECIDER_LANES") ? atoi(getenv("SVGPU_DECIDER_LANES")) : 48;
+  static const int phases = getenv("SVGPU_DECIDER_PHASES") ? atoi(getenv("SVGPU_DECIDER_PHASES")) : 3;
   const G1Aff* dl = reinterpret_cast<const G1Aff*>(d_lhs);
   const G1Aff* dr = reinterpret_cast<const G1Aff*>(d_rhs);
   const int mont = form == SV_MONTGOMERY ? 1 : 0;
   const LineCoeff* L2 = lines + ATE_NUM_LINES;
-  if (lanes == 1)
-    hipLaunchKernelGGL(k_decide, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, dl, dr, (uint32_t)n, lines, L2,
-                       mont, d_verdict, d_gt);
-  else if (lanes == 6)
-    hipLaunchKernelGGL(k_decide_lanes<1>, dim3((unsigned)((n + 7) / 8)), dim3(64), 0, st, dl, dr, (uint32_t)n,
-                       lines, L2, mont, d_verdict, d_gt);
-  else if (lanes == 12)
-    hipLaunchKernelGGL(k_decide_lanes<2>, dim3((unsigned)((n + 3) / 4)), dim3(64), 0, st, dl, dr, (uint32_t)n,
-                       lines, L2, mont, d_verdict, d_gt);
+  if (lanes == 48)
+    hipLaunchKernelGGL(k_decide_lanes<8>, dim3((unsigned)n), dim3(64), 0, st, dl, dr, (uint32_t)n, lines, L2, mont,
+                       d_verdict, d_gt, phases);
   else
     hipLaunchKernelGGL(k_decide_lanes<4>, dim3((unsigned)((n + 1) / 2)), dim3(64), 0, st, dl, dr, (uint32_t)n,
-                       lines, L2, mont, d_verdict, d_gt);
+                       lines, L2, mont, d_verdict, d_gt, phases);
   SV_HIP(hipGetLastError());
   SV_HIP(hipEventRecord(ws->ev[1], st));
   int32_t* hv = reinterpret_cast<int32_t*>(ws->pinned);

@@ -102,6 +102,27 @@ int sv_bn254_kzg_accumulate(const sv_g1_affine* lhs, const sv_g1_affine* rhs, si
                             const sv_fe* r, int form, int num_gpus, sv_g1_affine* out_lhs,
                             sv_g1_affine* out_rhs) SV_NOEXCEPT;
 
+/* ---- Poseidon sponge over BN254 Fr --------------------------
+ * x^5 HADES permutation, width t = 3 (R_F 8, R_P 57, rate 2: the SDK's PoseidonTranscript,
+ * snark-verifier-sdk/src/halo2.rs:52-71) or t = 5 (R_F 8, R_P 60, rate 4).  States are t
+ * consecutive sv_fe; inputs must be reduced field elements.
+ * permute: the bare HADES permutation of n states, in place: Poseidon::permutation
+ *          (snark-verifier/src/util/hash/poseidon.rs:469-500) called with a full-rate zero
+ *          input, exactly as the reference KATs call it (poseidon/tests.rs:34-85).
+ * squeeze: Poseidon::squeeze (poseidon.rs:455-467) on n independent sponges.  states (n x t,
+ *          in/out) are the sponges' states -- Poseidon::new starts one at (2^64, 0, ..),
+ *          poseidon.rs:335-342 -- and sponge j's buffer (what Poseidon::update collected,
+ *          poseidon.rs:449-452) is elements[offsets[j] .. offsets[j+1]); offsets has n + 1
+ *          non-decreasing entries.  out[j] (optional, may be NULL) = the challenge state[1].  */
+int sv_bn254_poseidon_permute(sv_fe* states, size_t n, int t, int form) SV_NOEXCEPT;
+int sv_bn254_poseidon_permute_device(sv_fe* d_states, size_t n, int t, int form, int device,
+                                     void* stream) SV_NOEXCEPT;
+int sv_bn254_poseidon_squeeze(sv_fe* states, const sv_fe* elements, const uint64_t* offsets,
+                              size_t n, int t, int form, sv_fe* out) SV_NOEXCEPT;
+int sv_bn254_poseidon_squeeze_device(sv_fe* d_states, const sv_fe* d_elements,
+                                     const uint64_t* d_offsets, size_t n, int t, int form,
+                                     sv_fe* d_out, int device, void* stream) SV_NOEXCEPT;
+
 /* ---- synthetic inputs (SURVEY.md section 8d generator, index-addressable) -------------
  * Fills device buffers with the deterministic SplitMix64 scalars / try-and-increment bases
  * (elements start .. start+n-1) in the requested form.                                   */

@@ -19,10 +19,22 @@ not vendored.  This module restates that published generator:
 * Permutation: R_F/2 full rounds, R_P partial rounds (S-box on state[0]), R_F/2 full
   rounds; each round = add constants, S-box x^5, MDS.  This is the unoptimised HADES
   form; the reference's optimised form (poseidon.rs:414-500) computes the same map.
+
+``Sponge`` restates the reference's sponge, Poseidon<F, L, T, RATE> (poseidon.rs:412-500):
+state starts (2^64, 0, ..) (State::default, :335-342); ``update`` buffers; ``squeeze``
+absorbs RATE-chunks (each added into state[1..], a short chunk padded with a single 1 --
+absorb_with_pre_constants, :363-385 -- then permuted), runs one extra permutation of the
+padded empty chunk when the buffer length is a multiple of RATE, and returns state[1].
+The reference holds no sponge-level vectors: that part is pinned only through the KAT-pinned
+permutation plus this line-by-line restatement (parity unpinned at the sponge level).
+``transcript_*`` restate PoseidonTranscript<NativeLoader> (system/halo2/transcript/halo2.rs:
+198-227): common_scalar = update([s]); common_ec_point = update([x mod r, y mod r])
+(fe_to_fe, util/arithmetic.rs:256-258), identity rejected; squeeze_challenge = squeeze().
 """
 from __future__ import annotations
 
-from typing import List
+import functools
+from typing import List, Optional, Sequence
 
 from .bn254 import R as FR_MODULUS
 
@@ -59,6 +71,7 @@ class Grain:
         return v
 
 
+@functools.lru_cache(maxsize=None)
 def spec(t: int, r_f: int, r_p: int, modulus: int = FR_MODULUS):
     n = modulus.bit_length()
     g = Grain(n, t, r_f, r_p)
@@ -90,3 +103,47 @@ def permutation(state: List[int], t: int, r_f: int, r_p: int, modulus: int = FR_
             st[0] = pow(st[0], 5, modulus)
         st = [sum(mds[i][j] * st[j] for j in range(t)) % modulus for i in range(t)]
     return st
+
+
+# widths the reference instantiates: t -> (R_F, R_P)  (tests.rs:39-42, :63-66; sdk halo2.rs:52-55)
+PARAMS = {3: (8, 57), 5: (8, 60)}
+
+
+class Sponge:
+    """Poseidon<Fr, Fr, T, RATE> on the NativeLoader (poseidon.rs:412-500)."""
+
+    def __init__(self, t: int = 3, state: Optional[Sequence[int]] = None):
+        self.t = t
+        self.r_f, self.r_p = PARAMS[t]
+        self.rate = t - 1
+        self.state = list(state) if state is not None else [1 << 64] + [0] * (t - 1)
+        self.buf: List[int] = []
+
+    def clear(self) -> None:
+        self.state = [1 << 64] + [0] * (self.t - 1)
+        self.buf = []
+
+    def update(self, elements: Sequence[int]) -> None:
+        self.buf.extend(int(e) % FR_MODULUS for e in elements)
+
+    def _permutation(self, inputs: Sequence[int]) -> None:
+        st = list(self.state)
+        for k, x in enumerate(inputs):
+            st[1 + k] += x
+        if len(inputs) < self.rate:
+            st[1 + len(inputs)] += 1
+        self.state = permutation(st, self.t, self.r_f, self.r_p)
+
+    def squeeze(self) -> int:
+        buf, self.buf = self.buf, []
+        for i in range(0, len(buf), self.rate):
+            self._permutation(buf[i:i + self.rate])
+        if len(buf) % self.rate == 0:
+            self._permutation([])
+        return self.state[1]
+
+
+def transcript_common_ec_point(sponge: Sponge, point) -> None:
+    if point is None:
+        raise ValueError("Invalid elliptic curve point encoding in proof")
+    sponge.update([point[0] % FR_MODULUS, point[1] % FR_MODULUS])

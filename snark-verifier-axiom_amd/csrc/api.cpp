@@ -13,6 +13,7 @@
 #include "gen.hpp"
 #include "host_ec.hpp"
 #include "msm.hpp"
+#include "poseidon.hpp"
 #include "runtime.hpp"
 
 using namespace sv;
@@ -308,6 +309,84 @@ int sv_bn254_kzg_accumulate(const sv_g1_affine* lhs, const sv_g1_affine* rhs, si
   affine_out(a, form, out_lhs);
   affine_out(b, form, out_rhs);
   return SV_OK;
+  SV_GUARD_END
+}
+
+int sv_bn254_poseidon_permute(sv_fe* states, size_t n, int t, int form) noexcept {
+  SV_GUARD_BEGIN
+  SV_TRY(check_form(form));
+  if (t != 3 && t != 5) {
+    sv::set_error("poseidon: unsupported width t = %d (3 or 5)", t);
+    return SV_ERR_ARG;
+  }
+  if (n == 0) return SV_OK;
+  if (!states) return SV_ERR_ARG;
+  if (resolve_gpus(1) == 0) return SV_ERR_DEVICE;
+  const int dev = runtime_device_id(0);
+  const size_t bytes = n * (size_t)t * sizeof(sv_fe);
+  DevBuf d;
+  SV_TRY(d.alloc(dev, bytes));
+  SV_HIP(hipMemcpy(d.p, states, bytes, hipMemcpyHostToDevice));
+  SV_TRY(poseidon_permute_device(d.p, n, t, form, nullptr));
+  SV_HIP(hipMemcpy(states, d.p, bytes, hipMemcpyDeviceToHost));
+  return SV_OK;
+  SV_GUARD_END
+}
+
+int sv_bn254_poseidon_permute_device(sv_fe* d_states, size_t n, int t, int form, int device, void* stream) noexcept {
+  SV_GUARD_BEGIN
+  SV_TRY(check_form(form));
+  if (resolve_gpus(0) == 0) return SV_ERR_DEVICE;
+  SV_HIP(hipSetDevice(device));
+  return poseidon_permute_device(d_states, n, t, form, (hipStream_t)stream);
+  SV_GUARD_END
+}
+
+int sv_bn254_poseidon_squeeze(sv_fe* states, const sv_fe* elements, const uint64_t* offsets, size_t n, int t,
+                              int form, sv_fe* out) noexcept {
+  SV_GUARD_BEGIN
+  SV_TRY(check_form(form));
+  if (t != 3 && t != 5) {
+    sv::set_error("poseidon: unsupported width t = %d (3 or 5)", t);
+    return SV_ERR_ARG;
+  }
+  if (n == 0) return SV_OK;
+  if (!states || !offsets) return SV_ERR_ARG;
+  for (size_t j = 0; j < n; j++)
+    if (offsets[j + 1] < offsets[j]) {
+      sv::set_error("poseidon: offsets not non-decreasing at %zu", j);
+      return SV_ERR_ARG;
+    }
+  const uint64_t total = offsets[n] - offsets[0];
+  if (total && !elements) return SV_ERR_ARG;
+  if (resolve_gpus(1) == 0) return SV_ERR_DEVICE;
+  const int dev = runtime_device_id(0);
+  // rebase offsets so only elements[offsets[0] .. offsets[n]) travel
+  std::vector<uint64_t> off(offsets, offsets + n + 1);
+  for (auto& o : off) o -= offsets[0];
+  const size_t sbytes = n * (size_t)t * sizeof(sv_fe);
+  DevBuf ds, de, doff, dout;
+  SV_TRY(ds.alloc(dev, sbytes));
+  SV_TRY(de.alloc(dev, total * sizeof(sv_fe)));
+  SV_TRY(doff.alloc(dev, (n + 1) * sizeof(uint64_t)));
+  SV_TRY(dout.alloc(dev, n * sizeof(sv_fe)));
+  SV_HIP(hipMemcpy(ds.p, states, sbytes, hipMemcpyHostToDevice));
+  if (total) SV_HIP(hipMemcpy(de.p, elements + offsets[0], total * sizeof(sv_fe), hipMemcpyHostToDevice));
+  SV_HIP(hipMemcpy(doff.p, off.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
+  SV_TRY(poseidon_squeeze_device(ds.p, de.p, static_cast<const uint64_t*>(doff.p), n, t, form, dout.p, nullptr));
+  SV_HIP(hipMemcpy(states, ds.p, sbytes, hipMemcpyDeviceToHost));
+  if (out) SV_HIP(hipMemcpy(out, dout.p, n * sizeof(sv_fe), hipMemcpyDeviceToHost));
+  return SV_OK;
+  SV_GUARD_END
+}
+
+int sv_bn254_poseidon_squeeze_device(sv_fe* d_states, const sv_fe* d_elements, const uint64_t* d_offsets, size_t n,
+                                     int t, int form, sv_fe* d_out, int device, void* stream) noexcept {
+  SV_GUARD_BEGIN
+  SV_TRY(check_form(form));
+  if (resolve_gpus(0) == 0) return SV_ERR_DEVICE;
+  SV_HIP(hipSetDevice(device));
+  return poseidon_squeeze_device(d_states, d_elements, d_offsets, n, t, form, d_out, (hipStream_t)stream);
   SV_GUARD_END
 }
 

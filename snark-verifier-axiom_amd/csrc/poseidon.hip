@@ -1,0 +1,188 @@
+// f2: the x^5 Poseidon sponge over BN254 Fr that drives PoseidonTranscript's Fiat-Shamir challenges
+// (snark-verifier/src/util/hash/poseidon.rs, system/halo2/transcript/halo2.rs:198-227).
+//
+// One lane per state.  The reference runs the "optimized" HADES schedule (poseidon.rs:121-208:
+// round-0 constants fused into absorb, sparse partial-round matrices); that schedule computes the
+// same map as the plain ARC -> S-box -> MDS rounds below, whose constants come from the Grain-LFSR
+// restatement in oracle/poseidon.py (pinned by the reference's permutation KATs, tests.rs:34-85)
+// and are compiled in as Montgomery limbs (poseidon_consts.hpp).  All constant loads are
+// wave-uniform (scalar loads); each lane's state stays in VGPRs.
+#include <hip/hip_runtime.h>
+
+#include "field.hpp"
+#include "poseidon.hpp"
+#include "poseidon_consts.hpp"
+#include "runtime.hpp"
+
+namespace sv {
+
+__constant__ uint32_t c_rc3[] = SV_POSEIDON_T3_RC_INIT;
+__constant__ uint32_t c_mds3[] = SV_POSEIDON_T3_MDS_INIT;
+__constant__ uint32_t c_rc5[] = SV_POSEIDON_T5_RC_INIT;
+__constant__ uint32_t c_mds5[] = SV_POSEIDON_T5_MDS_INIT;
+
+template <int T>
+struct PSpec;
+template <>
+struct PSpec<3> {
+  static constexpr int RF = SV_POSEIDON_T3_RF, RP = SV_POSEIDON_T3_RP;
+  static __device__ __forceinline__ const uint32_t* rc() { return c_rc3; }
+  static __device__ __forceinline__ const uint32_t* mds() { return c_mds3; }
+};
+template <>
+struct PSpec<5> {
+  static constexpr int RF = SV_POSEIDON_T5_RF, RP = SV_POSEIDON_T5_RP;
+  static __device__ __forceinline__ const uint32_t* rc() { return c_rc5; }
+  static __device__ __forceinline__ const uint32_t* mds() { return c_mds5; }
+};
+
+__device__ __forceinline__ Fr ld_const(const uint32_t* p) {
+  Fr r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = p[i];
+  return r;
+}
+
+__device__ __forceinline__ Fr pow5(const Fr& x) {
+  const Fr x2 = fe_sqr(x);
+  return fe_sqr(x2) * x;
+}
+
+// poseidon.rs:121-161 (permutation) == tests.rs's HADES reference: R_F/2 full, R_P partial, R_F/2 full.
+template <int T>
+__device__ __forceinline__ void permute(Fr (&s)[T]) {
+  constexpr int RF = PSpec<T>::RF, RP = PSpec<T>::RP;
+  const uint32_t* rc = PSpec<T>::rc();
+  const uint32_t* mds = PSpec<T>::mds();
+  for (int r = 0; r < RF + RP; r++) {
+#pragma unroll
+    for (int i = 0; i < T; i++) s[i] = s[i] + ld_const(rc + (r * T + i) * 8);
+    if (r < RF / 2 || r >= RF / 2 + RP) {
+#pragma unroll
+      for (int i = 0; i < T; i++) s[i] = pow5(s[i]);
+    } else {
+      s[0] = pow5(s[0]);
+    }
+    Fr o[T];
+#pragma unroll
+    for (int i = 0; i < T; i++) {
+      Fr acc = s[0] * ld_const(mds + (i * T) * 8);
+#pragma unroll
+      for (int j = 1; j < T; j++) acc = acc + s[j] * ld_const(mds + (i * T + j) * 8);
+      o[i] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < T; i++) s[i] = o[i];
+  }
+}
+
+__device__ __forceinline__ Fr load_fr(const Fr* p, int mont) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  const uint4 a = q[0], b = q[1];
+  Fr r;
+  r.v[0] = a.x, r.v[1] = a.y, r.v[2] = a.z, r.v[3] = a.w;
+  r.v[4] = b.x, r.v[5] = b.y, r.v[6] = b.z, r.v[7] = b.w;
+  return mont ? r : fe_to_mont(r);
+}
+
+__device__ __forceinline__ void store_fr(Fr* p, Fr v, int mont) {
+  if (!mont) v = fe_from_mont(v);
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = make_uint4(v.v[0], v.v[1], v.v[2], v.v[3]);
+  q[1] = make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]);
+}
+
+template <int T>
+__global__ void __launch_bounds__(256) k_poseidon_permute(Fr* __restrict__ st, uint32_t n, int mont) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Fr s[T];
+#pragma unroll
+  for (int k = 0; k < T; k++) s[k] = load_fr(st + (size_t)i * T + k, mont);
+  permute<T>(s);
+#pragma unroll
+  for (int k = 0; k < T; k++) store_fr(st + (size_t)i * T + k, s[k], mont);
+}
+
+// Poseidon::squeeze (poseidon.rs:455-467) for n independent sponges: sponge j's state (t elements,
+// in/out; Poseidon::new starts it at (2^64, 0, ..), poseidon.rs:335-342) absorbs its buffered
+// elements el[off[j] .. off[j+1]) RATE at a time: each chunk is added into state[1..], a chunk
+// shorter than RATE is padded with a single 1 (absorb_with_pre_constants, poseidon.rs:363-385),
+// and the state is permuted; when the buffer length is a multiple of RATE (including 0) one more
+// permutation runs on the padded empty chunk.  The challenge is state[1].  Elements must be reduced
+// field elements (halo2curves' Fr always is; the Python mirror reduces its ints mod r).
+template <int T>
+__global__ void __launch_bounds__(256) k_poseidon_squeeze(Fr* __restrict__ st, const Fr* __restrict__ el,
+                                                         const uint64_t* __restrict__ off, uint32_t n, int mont,
+                                                         Fr* __restrict__ out) {
+  constexpr int RATE = T - 1;
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint64_t b = off[j], e = off[j + 1];
+  Fr s[T];
+#pragma unroll
+  for (int k = 0; k < T; k++) s[k] = load_fr(st + (size_t)j * T + k, mont);
+  uint64_t p = b;
+  while (p < e) {
+    const uint64_t m = e - p < (uint64_t)RATE ? e - p : (uint64_t)RATE;
+#pragma unroll
+    for (int k = 0; k < RATE; k++) {
+      if ((uint64_t)k < m) s[k + 1] = s[k + 1] + load_fr(el + p + k, mont);
+      if ((uint64_t)k == m) s[k + 1] = s[k + 1] + Fr::one();  // 10* padding of a short chunk
+    }
+    permute<T>(s);
+    p += m;
+  }
+  if ((e - b) % RATE == 0) {  // exact: one more permutation of the padded empty chunk
+    s[1] = s[1] + Fr::one();
+    permute<T>(s);
+  }
+#pragma unroll
+  for (int k = 0; k < T; k++) store_fr(st + (size_t)j * T + k, s[k], mont);
+  if (out) store_fr(out + j, s[1], mont);
+}
+
+int poseidon_permute_device(void* d_states, size_t n, int t, int form, hipStream_t st) {
+  if (n == 0) return SV_OK;
+  if (n > 0xffffffffull) {
+    set_error("poseidon: n = %zu exceeds 2^32 - 1", n);
+    return SV_ERR_LEN;
+  }
+  const uint32_t blocks = (uint32_t)((n + 255) / 256);
+  Fr* s = static_cast<Fr*>(d_states);
+  if (t == 3)
+    hipLaunchKernelGGL(k_poseidon_permute<3>, dim3(blocks), dim3(256), 0, st, s, (uint32_t)n, form);
+  else if (t == 5)
+    hipLaunchKernelGGL(k_poseidon_permute<5>, dim3(blocks), dim3(256), 0, st, s, (uint32_t)n, form);
+  else {
+    set_error("poseidon: unsupported width t = %d (3 or 5)", t);
+    return SV_ERR_ARG;
+  }
+  SV_HIP(hipGetLastError());
+  return SV_OK;
+}
+
+int poseidon_squeeze_device(void* d_states, const void* d_elements, const uint64_t* d_offsets, size_t n, int t,
+                           int form, void* d_out, hipStream_t st) {
+  if (n == 0) return SV_OK;
+  if (n > 0xffffffffull) {
+    set_error("poseidon: n = %zu exceeds 2^32 - 1", n);
+    return SV_ERR_LEN;
+  }
+  const uint32_t blocks = (uint32_t)((n + 255) / 256);
+  Fr* s = static_cast<Fr*>(d_states);
+  const Fr* e = static_cast<const Fr*>(d_elements);
+  Fr* o = static_cast<Fr*>(d_out);
+  if (t == 3)
+    hipLaunchKernelGGL(k_poseidon_squeeze<3>, dim3(blocks), dim3(256), 0, st, s, e, d_offsets, (uint32_t)n, form, o);
+  else if (t == 5)
+    hipLaunchKernelGGL(k_poseidon_squeeze<5>, dim3(blocks), dim3(256), 0, st, s, e, d_offsets, (uint32_t)n, form, o);
+  else {
+    set_error("poseidon: unsupported width t = %d (3 or 5)", t);
+    return SV_ERR_ARG;
+  }
+  SV_HIP(hipGetLastError());
+  return SV_OK;
+}
+
+}  // namespace sv

@@ -84,3 +84,30 @@ def decide(g2, s_g2, lhs: torch.Tensor, rhs: torch.Tensor, form: int = _lib.SV_C
         ctypes.cast(gt, ctypes.c_void_p) if gt is not None else None), "sv_bn254_kzg_decide_device")
     gts = [enc.fq12_from_struct(g) for g in gt] if gt is not None else None
     return ff.value, list(verdicts), gts
+
+
+def poseidon_squeeze(states: torch.Tensor, elements: torch.Tensor, offsets: torch.Tensor, t: int = 3,
+                     form: int = _lib.SV_MONTGOMERY, out: torch.Tensor = None) -> torch.Tensor:
+    """Poseidon::squeeze on n HBM-resident sponges (states: (n * t, 4) int64 limbs, in/out;
+    elements: (m, 4); offsets: (n + 1,) int64, sponge j absorbs elements[offsets[j]:offsets[j+1]]).
+    Returns out (n, 4): the challenges."""
+    n = offsets.shape[0] - 1
+    if states.shape[0] != n * t:
+        raise _lib.LengthError(f"poseidon: {states.shape[0]} state rows for {n} sponges of width {t}")
+    if out is None:
+        out = torch.empty((max(n, 1), 4), dtype=torch.int64, device=states.device)
+    d = _dev_index(states)
+    _lib.check(_lib.lib.sv_bn254_poseidon_squeeze_device(states.data_ptr(), elements.data_ptr(), offsets.data_ptr(),
+                                                         n, t, form, out.data_ptr(), d,
+                                                         _stream_handle(states.device)),
+               "sv_bn254_poseidon_squeeze_device")
+    return out[:n]
+
+
+def poseidon_permute(states: torch.Tensor, t: int = 3, form: int = _lib.SV_MONTGOMERY) -> torch.Tensor:
+    """In-place HADES permutation of (n * t, 4) HBM-resident states."""
+    d = _dev_index(states)
+    _lib.check(_lib.lib.sv_bn254_poseidon_permute_device(states.data_ptr(), states.shape[0] // t, t, form, d,
+                                                         _stream_handle(states.device)),
+               "sv_bn254_poseidon_permute_device")
+    return states

@@ -78,3 +78,22 @@ def test_compute_without_gpu_fails_loudly():
     import svgpu
     with pytest.raises(svgpu.DeviceError):
         svgpu.multi_scalar_multiplication([1], [b.G1_GEN])
+
+
+def test_poseidon_arguments_rejected_without_compute():
+    from svgpu import _lib, poseidon as gp
+    buf = np.zeros(16, np.uint64)
+    off = np.zeros(2, np.uint64)
+    assert _lib.lib.sv_bn254_poseidon_permute(buf.ctypes.data, 1, 4, 0) == _lib.SV_ERR_ARG
+    assert _lib.lib.sv_bn254_poseidon_permute(buf.ctypes.data, 1, 3, 9) == _lib.SV_ERR_ARG
+    assert _lib.lib.sv_bn254_poseidon_permute(buf.ctypes.data, 0, 3, 0) == _lib.SV_OK  # nothing to do
+    bad = np.array([2, 1], np.uint64)
+    assert _lib.lib.sv_bn254_poseidon_squeeze(buf.ctypes.data, buf.ctypes.data, bad.ctypes.data, 1, 3, 0,
+                                              None) == _lib.SV_ERR_ARG
+    assert _lib.lib.sv_bn254_poseidon_squeeze(None, buf.ctypes.data, off.ctypes.data, 1, 3, 0,
+                                              None) == _lib.SV_ERR_ARG
+    with pytest.raises(_lib.ArgumentError):
+        gp.Poseidon(4)
+    with pytest.raises(_lib.LengthError):
+        gp.permute([[1, 2]], 3)
+    assert gp.permute([], 3) == [] and gp.squeeze_many([]) == []

@@ -102,3 +102,28 @@ def test_limb_codec_roundtrip():
     limbs = b.fe_to_limbs(x)
     assert all(l < (1 << 88) for l in limbs)
     assert b.fe_from_limbs(limbs) == x
+
+
+def test_poseidon_sponge_restatement_structure():
+    """Sponge (poseidon.rs:412-467): padding and the exact-length extra permutation, checked by
+    composing the KAT-pinned permutation by hand."""
+    t, (rf, rp) = 3, poseidon.PARAMS[3]
+    perm = lambda s: poseidon.permutation(s, t, rf, rp)  # noqa: E731
+    s0 = [1 << 64, 0, 0]
+    # empty buffer: one permutation of the padded empty chunk (state[1] += 1)
+    sp = poseidon.Sponge(t)
+    assert sp.squeeze() == perm([s0[0], 1, 0])[1]
+    # one element: chunk [a] padded with 1 at state[2]; not exact -> no extra permutation
+    sp = poseidon.Sponge(t)
+    sp.update([5])
+    assert sp.squeeze() == perm([s0[0], 5, 1])[1]
+    # two elements (exact): full chunk, then the padded empty chunk
+    sp = poseidon.Sponge(t)
+    sp.update([5, 6])
+    st = perm([s0[0], 5, 6])
+    assert sp.squeeze() == perm([st[0], st[1] + 1, st[2]])[1]
+    # inputs are reduced mod r like Fr
+    a, c = poseidon.Sponge(t), poseidon.Sponge(t)
+    a.update([3])
+    c.update([3 + poseidon.FR_MODULUS])
+    assert a.squeeze() == c.squeeze()

@@ -102,6 +102,23 @@ int sv_bn254_kzg_accumulate(const sv_g1_affine* lhs, const sv_g1_affine* rhs, si
                             const sv_fe* r, int form, int num_gpus, sv_g1_affine* out_lhs,
                             sv_g1_affine* out_rhs) SV_NOEXCEPT;
 
+/* ---- batched small MSMs -------------------------------------
+ * count independent MSMs over shared arrays: MSM k = sum_{i in [offsets[k], offsets[k+1])}
+ * scalars[i] * bases[i]; offsets has count + 1 non-decreasing entries; out[k] affine in
+ * `form`.  The per-proof Msm::evaluate calls of a native verifier (bdfg21.rs:75-78,
+ * gwc19.rs:76-79 -> native.rs:61-71) and the two accumulation MSMs of KzgAs::create_proof
+ * (accumulation.rs:177-192) in one launch.  An empty MSM is SV_ERR_EMPTY ("pairs should not
+ * be empty", native.rs:69).  Host API: MSMs above SVGPU_BATCH_MAX terms (default 4096), and
+ * every MSM of a batch of at most SVGPU_BATCH_SEQ_MAX (default 4), run through the single-MSM
+ * pipeline instead.  Device API: every MSM runs in the batch kernel
+ * (max_terms = the largest MSM, picks the window size); synchronous on `stream`.          */
+int sv_bn254_g1_msm_batch(const sv_g1_affine* bases, const sv_fe* scalars, const uint64_t* offsets,
+                          size_t count, int form, sv_g1_affine* out) SV_NOEXCEPT;
+int sv_bn254_g1_msm_batch_device(const sv_g1_affine* d_bases, const sv_fe* d_scalars,
+                                 const uint64_t* d_offsets, size_t count, size_t max_terms,
+                                 int form, int device, void* stream,
+                                 sv_g1_affine* d_out) SV_NOEXCEPT;
+
 /* ---- Poseidon sponge over BN254 Fr --------------------------
  * x^5 HADES permutation, width t = 3 (R_F 8, R_P 57, rate 2: the SDK's PoseidonTranscript,
  * snark-verifier-sdk/src/halo2.rs:52-71) or t = 5 (R_F 8, R_P 60, rate 4).  States are t

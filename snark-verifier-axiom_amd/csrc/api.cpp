@@ -3,6 +3,8 @@
 // points need a GPU and return SV_ERR_DEVICE without one.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <thread>
@@ -13,6 +15,7 @@
 #include "gen.hpp"
 #include "host_ec.hpp"
 #include "msm.hpp"
+#include "msm_batch.hpp"
 #include "poseidon.hpp"
 #include "runtime.hpp"
 
@@ -309,6 +312,86 @@ int sv_bn254_kzg_accumulate(const sv_g1_affine* lhs, const sv_g1_affine* rhs, si
   affine_out(a, form, out_lhs);
   affine_out(b, form, out_rhs);
   return SV_OK;
+  SV_GUARD_END
+}
+
+int sv_bn254_g1_msm_batch(const sv_g1_affine* bases, const sv_fe* scalars, const uint64_t* offsets, size_t count,
+                          int form, sv_g1_affine* out) noexcept {
+  SV_GUARD_BEGIN
+  SV_TRY(check_form(form));
+  if (count == 0) return SV_OK;
+  if (!offsets || !out) return SV_ERR_ARG;
+  for (size_t k = 0; k < count; k++) {
+    if (offsets[k + 1] < offsets[k]) {
+      sv::set_error("msm_batch: offsets not non-decreasing at %zu", k);
+      return SV_ERR_ARG;
+    }
+    if (offsets[k + 1] == offsets[k]) {
+      sv::set_error("pairs should not be empty (msm %zu)", k);
+      return SV_ERR_EMPTY;
+    }
+  }
+  if (!bases || !scalars) return SV_ERR_ARG;
+  if (count > 0x7fffffffull) return SV_ERR_LEN;
+  if (resolve_gpus(1) == 0) return SV_ERR_DEVICE;
+  const int dev = runtime_device_id(0);
+  size_t big_limit = 4096;
+  if (const char* e = getenv("SVGPU_BATCH_MAX")) big_limit = strtoull(e, nullptr, 10);
+  const uint64_t base = offsets[0], total = offsets[count] - base;
+  std::vector<uint64_t> off(offsets, offsets + count + 1);
+  for (auto& o : off) o -= base;
+  // The batch kernel costs about one Horner chain (~2 ms) whatever the batch size; the single-MSM
+  // pipeline finishes its (host-side) Horner in ~0.35 ms per MSM.  Tiny batches go sequential.
+  size_t seq_max = 4;
+  if (const char* e = getenv("SVGPU_BATCH_SEQ_MAX")) seq_max = strtoull(e, nullptr, 10);
+  if (count <= seq_max) big_limit = 0;
+  std::vector<uint32_t> small_ids, big_ids;
+  size_t max_small = 0;
+  for (size_t k = 0; k < count; k++) {
+    const size_t m = off[k + 1] - off[k];
+    if (m > big_limit) {
+      big_ids.push_back((uint32_t)k);
+    } else {
+      small_ids.push_back((uint32_t)k);
+      max_small = std::max(max_small, m);
+    }
+  }
+  DevBuf db, ds, doff, dids, dout;
+  SV_TRY(db.alloc(dev, total * sizeof(sv_g1_affine)));
+  SV_TRY(ds.alloc(dev, total * sizeof(sv_fe)));
+  SV_TRY(doff.alloc(dev, (count + 1) * sizeof(uint64_t)));
+  SV_TRY(dids.alloc(dev, count * sizeof(uint32_t)));
+  SV_TRY(dout.alloc(dev, count * sizeof(sv_g1_affine)));
+  SV_HIP(hipMemcpy(db.p, bases + base, total * sizeof(sv_g1_affine), hipMemcpyHostToDevice));
+  SV_HIP(hipMemcpy(ds.p, scalars + base, total * sizeof(sv_fe), hipMemcpyHostToDevice));
+  SV_HIP(hipMemcpy(doff.p, off.data(), (count + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
+  if (!small_ids.empty()) {
+    SV_HIP(hipMemcpy(dids.p, small_ids.data(), small_ids.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    SV_TRY(msm_batch_device(db.p, ds.p, static_cast<const uint64_t*>(doff.p), static_cast<const uint32_t*>(dids.p),
+                            small_ids.size(), max_small, form, dev, nullptr, dout.p));
+    SV_HIP(hipMemcpy(out, dout.p, count * sizeof(sv_g1_affine), hipMemcpyDeviceToHost));
+  }
+  for (uint32_t k : big_ids) {
+    Xyzz r;
+    SV_TRY(msm_run_device(static_cast<const sv_g1_affine*>(db.p) + off[k], static_cast<const sv_fe*>(ds.p) + off[k],
+                          off[k + 1] - off[k], form, dev, nullptr, &r));
+    affine_out(r, form, &out[k]);
+  }
+  return SV_OK;
+  SV_GUARD_END
+}
+
+int sv_bn254_g1_msm_batch_device(const sv_g1_affine* d_bases, const sv_fe* d_scalars, const uint64_t* d_offsets,
+                                 size_t count, size_t max_terms, int form, int device, void* stream,
+                                 sv_g1_affine* d_out) noexcept {
+  SV_GUARD_BEGIN
+  SV_TRY(check_form(form));
+  if (count == 0) return SV_OK;
+  if (!d_bases || !d_scalars || !d_offsets || !d_out) return SV_ERR_ARG;
+  if (resolve_gpus(0) == 0) return SV_ERR_DEVICE;
+  SV_HIP(hipSetDevice(device));
+  return msm_batch_device(d_bases, d_scalars, d_offsets, nullptr, count, max_terms, form, device, (hipStream_t)stream,
+                          d_out);
   SV_GUARD_END
 }
 

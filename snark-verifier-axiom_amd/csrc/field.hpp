@@ -337,25 +337,116 @@ SV_HD Fe<M> fe_from_mont(const Fe<M>& a) {
   return a * o;
 }
 
-// a^(m-2): Fermat inverse (0 -> 0).  Exponent bits of m-2 scanned MSB first.
+// Inverse in Montgomery form (0 -> 0) by the binary extended Euclidean algorithm (Guide to ECC,
+// alg. 2.22) on the raw integer aR: ~2 x 254 shift / subtract steps of plain integer VALU work,
+// about 5x shorter than the 254-squaring Fermat chain on one lane -- and inversions sit on serial
+// tails (affine conversion after a Horner chain, the decider's final exponentiation).  Inputs
+// are public (verifier data), so the data-dependent running time is harmless.
+// inv_raw(aR) = (aR)^-1; times R^3 (Montgomery) gives a^-1 R.
+namespace detail {
+SV_HD bool lw_is_one(const uint32_t* x) {
+  uint32_t acc = x[0] ^ 1u;
+#pragma unroll
+  for (int i = 1; i < 8; i++) acc |= x[i];
+  return acc == 0;
+}
+SV_HD void lw_shr1(uint32_t* x, uint32_t top) {
+#pragma unroll
+  for (int i = 0; i < 7; i++) x[i] = (x[i] >> 1) | (x[i + 1] << 31);
+  x[7] = (x[7] >> 1) | (top << 31);
+}
+// x = (x even ? x : x + m) / 2   (x < m < 2^255)
 template <class M>
-SV_NOINL Fe<M> fe_inv(const Fe<M>& a) {
-  uint32_t e[8];
-  uint64_t br = 2;
+SV_HD void lw_half_mod(uint32_t* x) {
+  if (x[0] & 1) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      c += (uint64_t)x[i] + M::p(i);
+      x[i] = (uint32_t)c;
+      c >>= 32;
+    }
+    lw_shr1(x, (uint32_t)c);
+  } else {
+    lw_shr1(x, 0);
+  }
+}
+SV_HD bool lw_ge(const uint32_t* a, const uint32_t* b) {
+  uint64_t br = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    uint64_t s = (uint64_t)M::p(i) - br;
-    e[i] = (uint32_t)s;
+    uint64_t s = (uint64_t)a[i] - b[i] - br;
     br = (s >> 63) & 1;
   }
-  Fe<M> r = Fe<M>::one();
-  for (int i = 7; i >= 0; i--) {
-    for (int b = 31; b >= 0; b--) {
-      r = fe_sqr(r);
-      if ((e[i] >> b) & 1) r = r * a;
+  return br == 0;
+}
+SV_HD void lw_sub(uint32_t* a, const uint32_t* b) {
+  uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t s = (uint64_t)a[i] - b[i] - br;
+    a[i] = (uint32_t)s;
+    br = (s >> 63) & 1;
+  }
+}
+// a = a - b mod m, a, b < m
+template <class M>
+SV_HD void lw_sub_mod(uint32_t* a, const uint32_t* b) {
+  uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t s = (uint64_t)a[i] - b[i] - br;
+    a[i] = (uint32_t)s;
+    br = (s >> 63) & 1;
+  }
+  if (br) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      c += (uint64_t)a[i] + M::p(i);
+      a[i] = (uint32_t)c;
+      c >>= 32;
     }
   }
-  return r;
+}
+}  // namespace detail
+
+template <class M>
+SV_NOINL Fe<M> fe_inv(const Fe<M>& a) {
+  if (a.is_zero()) return a;
+  uint32_t u[8], v[8], x1[8], x2[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    u[i] = a.v[i];
+    v[i] = M::p(i);
+    x1[i] = i == 0 ? 1u : 0u;
+    x2[i] = 0u;
+  }
+  // invariants: x1 * a == u, x2 * a == v (mod m); gcd(u, v) == 1
+  while (!detail::lw_is_one(u) && !detail::lw_is_one(v)) {
+    while (!(u[0] & 1)) {
+      detail::lw_shr1(u, 0);
+      detail::lw_half_mod<M>(x1);
+    }
+    while (!(v[0] & 1)) {
+      detail::lw_shr1(v, 0);
+      detail::lw_half_mod<M>(x2);
+    }
+    if (detail::lw_ge(u, v)) {
+      detail::lw_sub(u, v);
+      detail::lw_sub_mod<M>(x1, x2);
+    } else {
+      detail::lw_sub(v, u);
+      detail::lw_sub_mod<M>(x2, x1);
+    }
+  }
+  Fe<M> r, r2;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    r.v[i] = detail::lw_is_one(u) ? x1[i] : x2[i];
+    r2.v[i] = M::r2(i);
+  }
+  return r * (r2 * r2);  // (aR)^-1 * R^3 / R = a^-1 R
 }
 
 using Fq = Fe<FqTag>;

@@ -1,0 +1,387 @@
+// f1: many small MSMs in ONE launch: the per-proof MSMs of native
+// verification (bdfg21.rs:75-78, gwc19.rs:76-79 via Msm::evaluate -> NativeLoader::
+// multi_scalar_multiplication, native.rs:61-71) and the two accumulation MSMs of
+// KzgAs::create_proof (accumulation.rs:177-192) are tens to thousands of terms each -- far too
+// small to fill 256 CUs one at a time (the single-MSM pipeline is launch/latency bound there).
+//
+// One workgroup (256 threads) per MSM, everything in LDS, signed c-bit windows (c = 5 for small
+// batches, 8 for larger MSMs):
+//   1. chunk of NCH terms: scalars -> W signed digits (LDS), LDS-atomic histogram per (window,
+//      bucket), per-window exclusive scan, scatter of term indices into per-bucket lists;
+//   2. G = min(2^(c-1), 64) lanes per window: each lane sums its buckets' lists with mixed XYZZ
+//      adds, weights them by the bucket magnitude (short double-and-add), and the G lanes fold
+//      with xor-shuffles; the group leader adds the window sum into T[w] (LDS, kept across chunks);
+//   3. one wave per MSM: Horner over the windows (~255 doublings), the independent products of
+//      each doubling / addition spread over 4 lanes (3-4 product levels instead of 9-14), then
+//      one binary-EEA inversion, affine out.
+// Steps 1-2 run as (MSM, window group) blocks so even one MSM spreads over several CUs; step 3
+// is a dependent chain per MSM (one wave each), so a batch costs about one chain whatever its
+// size.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+
+#include "curve.hpp"
+#include "msm_batch.hpp"
+#include "runtime.hpp"
+
+namespace sv {
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ Fq ld_fq(const uint32_t* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  const uint4 a = q[0], b = q[1];
+  Fq r;
+  r.v[0] = a.x, r.v[1] = a.y, r.v[2] = a.z, r.v[3] = a.w;
+  r.v[4] = b.x, r.v[5] = b.y, r.v[6] = b.z, r.v[7] = b.w;
+  return r;
+}
+
+__device__ __forceinline__ void st_fq(uint32_t* p, const Fq& v) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = make_uint4(v.v[0], v.v[1], v.v[2], v.v[3]);
+  q[1] = make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]);
+}
+
+__device__ __forceinline__ Fq shfl_xor_fq(const Fq& a, int m) {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = (uint32_t)__shfl_xor((int)a.v[i], m);
+  return r;
+}
+
+__device__ __forceinline__ G1Xyzz shfl_xor_pt(const G1Xyzz& p, int m) {
+  return {shfl_xor_fq(p.X, m), shfl_xor_fq(p.Y, m), shfl_xor_fq(p.ZZ, m), shfl_xor_fq(p.ZZZ, m)};
+}
+
+// k * P for 1 <= k <= 128, MSB first
+__device__ __forceinline__ G1Xyzz smul_small(const G1Xyzz& p, uint32_t k) {
+  G1Xyzz r = p;
+  const int top = 31 - __clz(k);
+  for (int b = top - 1; b >= 0; b--) {
+    r = xyzz_dbl(r);
+    if ((k >> b) & 1) r = xyzz_add(r, p);
+  }
+  return r;
+}
+
+template <int C>
+struct BatchCfg {
+  static constexpr int W = (255 + C - 1) / C;  // signed digits of a < 2^254 scalar fit in 255 bits
+  static constexpr int B = 1 << (C - 1);
+  static constexpr int G = B < 64 ? B : 64;  // lanes per window
+  static constexpr int BPL = B / G;          // buckets per lane
+  static constexpr int WPB = kThreads / G;   // windows per block
+  static constexpr int WG = (W + WPB - 1) / WPB;  // window groups (blockIdx.y)
+  static constexpr int NCH = C <= 6 ? 128 : 256;
+};
+
+// Step 1 + 2: block (msm, window group) -> window sums Tg[id * W + w] (XYZZ, Montgomery).
+template <int C>
+__global__ void __launch_bounds__(kThreads) k_msm_batch_windows(const G1Aff* __restrict__ bases,
+                                                                 const Fr* __restrict__ scalars,
+                                                                 const uint64_t* __restrict__ off,
+                                                                 const uint32_t* __restrict__ ids, int mont,
+                                                                 G1Xyzz* __restrict__ Tg, uint32_t* __restrict__ err) {
+  using Cf = BatchCfg<C>;
+  constexpr int W = Cf::W, B = Cf::B, G = Cf::G, BPL = Cf::BPL, WPB = Cf::WPB, NCH = Cf::NCH;
+  __shared__ uint32_t cur[WPB * B];   // histogram, then scatter cursors (= bucket ends)
+  __shared__ uint16_t bst[WPB * B];   // bucket starts within the window's list
+  __shared__ uint16_t dig[NCH * WPB]; // magnitude | sign << 8
+  __shared__ uint16_t lst[WPB * NCH]; // term index | sign << 15
+  __shared__ G1Xyzz T[WPB];           // window sums of this block's windows
+
+  const int tid = threadIdx.x;
+  const uint32_t id = ids ? ids[blockIdx.x] : blockIdx.x;  // optional indirection (host API skips big MSMs)
+  const int w0 = blockIdx.y * WPB;
+  const int nw = W - w0 < WPB ? W - w0 : WPB;
+  const uint64_t b0 = off[id], e0 = off[id + 1];
+  if (tid < WPB) T[tid] = G1Xyzz::identity();
+
+  for (uint64_t c0 = b0; c0 < e0; c0 += NCH) {
+    const int m = (int)(e0 - c0 < (uint64_t)NCH ? e0 - c0 : (uint64_t)NCH);
+    for (int i = tid; i < WPB * B; i += kThreads) cur[i] = 0;
+    __syncthreads();
+    if (tid < m) {
+      Fr s;
+      {
+        const Fq t = ld_fq(reinterpret_cast<const uint32_t*>(scalars + c0 + tid));
+#pragma unroll
+        for (int i = 0; i < 8; i++) s.v[i] = t.v[i];
+      }
+      if (!s.is_reduced()) atomicOr(err, 2u);
+      if (mont) s = fe_from_mont(s);
+      // signed digits: the carry runs from window 0, only this block's windows are kept
+      uint32_t carry = 0;
+      for (int w = 0; w < w0 + nw; w++) {
+        const int pos = w * C, limb = pos >> 5, sh = pos & 31;
+        const uint32_t lo = limb < 8 ? s.v[limb] : 0u;
+        const uint32_t hi = limb + 1 < 8 ? s.v[limb + 1] : 0u;
+        uint32_t bits = sh ? ((lo >> sh) | (hi << (32 - sh))) : lo;
+        bits = (bits & ((1u << C) - 1)) + carry;
+        uint32_t mag, neg;
+        if (bits > (uint32_t)B) {  // digit bits - 2^C < 0 (bits == 2^C: digit 0, carry 1)
+          mag = (1u << C) - bits;
+          neg = mag ? 1u : 0u;
+          carry = 1;
+        } else {
+          mag = bits;
+          neg = 0;
+          carry = 0;
+        }
+        if (w >= w0) {
+          const int lw = w - w0;
+          dig[tid * WPB + lw] = (uint16_t)(mag | (neg << 8));
+          if (mag) atomicAdd(&cur[lw * B + mag - 1], 1u);
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < nw) {
+      uint32_t acc = 0;
+      for (int b = 0; b < B; b++) {
+        const uint32_t c = cur[tid * B + b];
+        bst[tid * B + b] = (uint16_t)acc;
+        cur[tid * B + b] = acc;
+        acc += c;
+      }
+    }
+    __syncthreads();
+    if (tid < m) {
+      for (int lw = 0; lw < nw; lw++) {
+        const uint32_t d = dig[tid * WPB + lw];
+        const uint32_t mag = d & 0xff;
+        if (mag) {
+          const uint32_t pos = atomicAdd(&cur[lw * B + mag - 1], 1u);
+          lst[lw * NCH + pos] = (uint16_t)(tid | ((d >> 8) << 15));
+        }
+      }
+    }
+    __syncthreads();
+    {
+      const int lw = tid / G;
+      const int g = tid % G;
+      G1Xyzz part = G1Xyzz::identity();
+      if (lw < nw) {
+        for (int k = 0; k < BPL; k++) {
+          const int b = g + k * G;  // magnitude b + 1
+          G1Xyzz acc = G1Xyzz::identity();
+          const uint32_t pe = cur[lw * B + b];
+          for (uint32_t p = bst[lw * B + b]; p < pe; p++) {
+            const uint32_t e = lst[lw * NCH + p];
+            const uint32_t* bp = reinterpret_cast<const uint32_t*>(bases + c0 + (e & 0x7fff));
+            Fq x = ld_fq(bp), y = ld_fq(bp + 8);
+            if (x.is_zero() && y.is_zero()) continue;  // identity base
+            if (!mont) {
+              x = fe_to_mont(x);
+              y = fe_to_mont(y);
+            }
+            if (e >> 15) y = -y;
+            acc = xyzz_madd(acc, x, y);
+          }
+          if (!acc.is_identity()) part = xyzz_add(part, smul_small(acc, (uint32_t)b + 1));
+        }
+      }
+#pragma unroll
+      for (int s = 1; s < G; s <<= 1) part = xyzz_add(part, shfl_xor_pt(part, s));
+      if (g == 0 && lw < nw) T[lw] = xyzz_add(T[lw], part);
+    }
+    __syncthreads();
+  }
+  if (tid < nw) Tg[(size_t)id * W + w0 + tid] = T[tid];
+}
+
+// ---- Step 3: Horner over the window sums with the independent products of each XYZZ doubling /
+// addition issued by up to 4 lanes of one wave at once (LDS slots; 3 product levels per
+// doubling instead of 9 products, 4 per addition instead of 14).  One wave per MSM.
+enum Slot {
+  sX, sY, sZZ, sZZZ,      // accumulator
+  tX, tY, tZZ, tZZZ,      // addend
+  sU, sV, sX2, sM, sW, sS, sMsq, sX3, sTm, sZZn, sZZZn, sWY, sMS,
+  sU1, sU2, sS1, sS2, sP, sR, sPP, sRR, sZ12, sZ123, sPPP, sQ,
+  kSlots
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// lanes 0..n-1: R[d_l] = R[a_l] * R[b_l]
+__device__ __forceinline__ void par_mul(Fq* R, int lane, int n, int a0, int b0, int d0, int a1 = 0, int b1 = 0,
+                                        int d1 = 0, int a2 = 0, int b2 = 0, int d2 = 0, int a3 = 0, int b3 = 0,
+                                        int d3 = 0) {
+  if (lane < n) {
+    const int a = lane == 0 ? a0 : lane == 1 ? a1 : lane == 2 ? a2 : a3;
+    const int b = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
+    const int d = lane == 0 ? d0 : lane == 1 ? d1 : lane == 2 ? d2 : d3;
+    const Fq r = R[a] * R[b];
+    R[d] = r;
+  }
+  wave_sync();
+}
+
+// dbl-2008-s-1 (same formulas as xyzz_dbl); identity (ZZ = 0) stays identity
+__device__ void par_dbl(Fq* R, int lane) {
+  if (lane == 0) R[sU] = fe_dbl(R[sY]);
+  wave_sync();
+  par_mul(R, lane, 2, sU, sU, sV, sX, sX, sX2);
+  if (lane == 0) R[sM] = fe_dbl(R[sX2]) + R[sX2];
+  wave_sync();
+  par_mul(R, lane, 4, sU, sV, sW, sX, sV, sS, sV, sZZ, sZZn, sM, sM, sMsq);
+  if (lane == 0) {
+    const Fq x3 = R[sMsq] - fe_dbl(R[sS]);
+    R[sX3] = x3;
+    R[sTm] = R[sS] - x3;
+  }
+  wave_sync();
+  par_mul(R, lane, 3, sW, sZZZ, sZZZn, sW, sY, sWY, sM, sTm, sMS);
+  if (lane == 0) {
+    R[sY] = R[sMS] - R[sWY];
+    R[sX] = R[sX3];
+    R[sZZ] = R[sZZn];
+    R[sZZZ] = R[sZZZn];
+  }
+  wave_sync();
+}
+
+// add-2008-s: acc += addend (slots t*), complete (identities, P == Q, P == -Q)
+__device__ void par_add(Fq* R, int lane) {
+  if (R[tZZ].is_zero()) return;  // LDS broadcast reads: uniform branches
+  if (R[sZZ].is_zero()) {
+    if (lane == 0) {
+      R[sX] = R[tX];
+      R[sY] = R[tY];
+      R[sZZ] = R[tZZ];
+      R[sZZZ] = R[tZZZ];
+    }
+    wave_sync();
+    return;
+  }
+  par_mul(R, lane, 4, sX, tZZ, sU1, tX, sZZ, sU2, sY, tZZZ, sS1, tY, sZZZ, sS2);
+  if (lane == 0) {
+    R[sP] = R[sU2] - R[sU1];
+    R[sR] = R[sS2] - R[sS1];
+  }
+  wave_sync();
+  if (R[sP].is_zero()) {
+    if (R[sR].is_zero()) {
+      par_dbl(R, lane);
+    } else {
+      if (lane == 0) R[sZZ] = R[sZZZ] = Fq::zero();
+      wave_sync();
+    }
+    return;
+  }
+  par_mul(R, lane, 4, sP, sP, sPP, sR, sR, sRR, sZZ, tZZ, sZ12, sZZZ, tZZZ, sZ123);
+  par_mul(R, lane, 3, sP, sPP, sPPP, sU1, sPP, sQ, sZ12, sPP, sZZn);
+  if (lane == 0) {
+    const Fq x3 = R[sRR] - R[sPPP] - fe_dbl(R[sQ]);
+    R[sX3] = x3;
+    R[sTm] = R[sQ] - x3;
+  }
+  wave_sync();
+  par_mul(R, lane, 3, sR, sTm, sMS, sS1, sPPP, sWY, sZ123, sPPP, sZZZn);
+  if (lane == 0) {
+    R[sY] = R[sMS] - R[sWY];
+    R[sX] = R[sX3];
+    R[sZZ] = R[sZZn];
+    R[sZZZ] = R[sZZZn];
+  }
+  wave_sync();
+}
+
+template <int C>
+__global__ void __launch_bounds__(64) k_msm_batch_horner(const G1Xyzz* __restrict__ Tg, const uint32_t* __restrict__ ids,
+                                                         int mont, G1Aff* __restrict__ out) {
+  constexpr int W = BatchCfg<C>::W;
+  __shared__ Fq R[kSlots];
+  const int lane = threadIdx.x;
+  const uint32_t id = ids ? ids[blockIdx.x] : blockIdx.x;
+  const G1Xyzz* T = Tg + (size_t)id * W;
+  if (lane == 0) {
+    const G1Xyzz t = T[W - 1];
+    R[sX] = t.X, R[sY] = t.Y, R[sZZ] = t.ZZ, R[sZZZ] = t.ZZZ;
+  }
+  wave_sync();
+  for (int w = W - 2; w >= 0; w--) {
+    for (int i = 0; i < C; i++) par_dbl(R, lane);
+    if (lane == 0) {
+      const G1Xyzz t = T[w];
+      R[tX] = t.X, R[tY] = t.Y, R[tZZ] = t.ZZ, R[tZZZ] = t.ZZZ;
+    }
+    wave_sync();
+    par_add(R, lane);
+  }
+  if (lane == 0) {
+    const G1Xyzz acc = {R[sX], R[sY], R[sZZ], R[sZZZ]};
+    G1Aff r = xyzz_to_affine(acc);
+    if (!mont && !acc.is_identity()) {
+      r.x = fe_from_mont(r.x);
+      r.y = fe_from_mont(r.y);
+    }
+    uint32_t* o = reinterpret_cast<uint32_t*>(out + id);
+    st_fq(o, r.x);
+    st_fq(o + 8, r.y);
+  }
+}
+
+}  // namespace
+
+int msm_batch_window_bits(size_t max_terms) {
+  if (const char* e = getenv("SVGPU_BATCH_WINDOW_BITS")) {
+    const int c = atoi(e);
+    if (c == 5 || c == 8) return c;
+  }
+  return max_terms <= 256 ? 5 : 8;
+}
+
+int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t* d_offsets, const uint32_t* d_ids,
+                     size_t count, size_t max_terms, int form, int device, hipStream_t stream, void* d_out) {
+  if (count == 0) return SV_OK;
+  if (count > 0x7fffffffull) {
+    set_error("msm_batch: count = %zu too large", count);
+    return SV_ERR_LEN;
+  }
+  WsLease lease(device, stream);
+  if (!lease.ok()) return SV_ERR_DEVICE;
+  Workspace* ws = lease.get();
+  hipStream_t st = ws->stream;
+  const int c = msm_batch_window_bits(max_terms);
+  const int W = c == 5 ? BatchCfg<5>::W : BatchCfg<8>::W;
+  const int WG = c == 5 ? BatchCfg<5>::WG : BatchCfg<8>::WG;
+  SV_TRY(ws->reserve(Workspace::aligned(4) + Workspace::aligned(count * W * sizeof(G1Xyzz))));
+  SV_TRY(ws->reserve_pinned(256));
+  uint32_t* err = ws->carve<uint32_t>(1);
+  G1Xyzz* Tg = ws->carve<G1Xyzz>(count * W);
+  SV_HIP(hipMemsetAsync(err, 0, 4, st));
+  const int mont = form == SV_MONTGOMERY;
+  const G1Aff* b = static_cast<const G1Aff*>(d_bases);
+  const Fr* s = static_cast<const Fr*>(d_scalars);
+  G1Aff* o = static_cast<G1Aff*>(d_out);
+  const dim3 grid((uint32_t)count, WG);
+  if (c == 5) {
+    hipLaunchKernelGGL(k_msm_batch_windows<5>, grid, dim3(kThreads), 0, st, b, s, d_offsets, d_ids, mont, Tg, err);
+    hipLaunchKernelGGL(k_msm_batch_horner<5>, dim3((uint32_t)count), dim3(64), 0, st, Tg, d_ids, mont, o);
+  } else {
+    hipLaunchKernelGGL(k_msm_batch_windows<8>, grid, dim3(kThreads), 0, st, b, s, d_offsets, d_ids, mont, Tg, err);
+    hipLaunchKernelGGL(k_msm_batch_horner<8>, dim3((uint32_t)count), dim3(64), 0, st, Tg, d_ids, mont, o);
+  }
+  SV_HIP(hipGetLastError());
+  SV_HIP(hipMemcpyAsync(ws->pinned, err, 4, hipMemcpyDeviceToHost, st));
+  SV_HIP(hipStreamSynchronize(st));
+  uint32_t ev;
+  memcpy(&ev, ws->pinned, 4);
+  if (ev & 2u) {
+    set_error("msm_batch: scalar not reduced (>= r)");
+    return SV_ERR_ARG;
+  }
+  return SV_OK;
+}
+
+}  // namespace sv

@@ -1,0 +1,16 @@
+// Batched small MSMs (see msm_batch.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace sv {
+// count MSMs; MSM k = sum over i in [off[k], off[k+1]) of scalars[i] * bases[i] (device arrays);
+// d_out[k] = affine result in `form`.  max_terms (the largest MSM) only picks the window size.
+// d_ids (optional): launch only MSMs d_ids[0..count) (results still land at d_out[id]).
+// Synchronous on `stream`.
+int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t* d_offsets, const uint32_t* d_ids,
+                     size_t count, size_t max_terms, int form, int device, hipStream_t stream, void* d_out);
+int msm_batch_window_bits(size_t max_terms);
+}  // namespace sv

@@ -94,6 +94,9 @@ PROTOTYPES = [
                                             c_size_t, c_int, c_int, c_void_p, POINTER(c_int32), c_void_p, c_void_p]),
     ("sv_bn254_kzg_accumulate", c_int, [c_void_p, c_void_p, c_size_t, POINTER(sv_fe), c_int, c_int,
                                          POINTER(sv_g1_affine), POINTER(sv_g1_affine)]),
+    ("sv_bn254_g1_msm_batch", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
+    ("sv_bn254_g1_msm_batch_device", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_int, c_int,
+                                              c_void_p, c_void_p]),
     ("sv_bn254_poseidon_permute", c_int, [c_void_p, c_size_t, c_int, c_int]),
     ("sv_bn254_poseidon_permute_device", c_int, [c_void_p, c_size_t, c_int, c_int, c_int, c_void_p]),
     ("sv_bn254_poseidon_squeeze", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p]),

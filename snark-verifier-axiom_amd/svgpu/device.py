@@ -111,3 +111,18 @@ def poseidon_permute(states: torch.Tensor, t: int = 3, form: int = _lib.SV_MONTG
                                                          _stream_handle(states.device)),
                "sv_bn254_poseidon_permute_device")
     return states
+
+
+def msm_batch(bases: torch.Tensor, scalars: torch.Tensor, offsets: torch.Tensor, max_terms: int,
+              form: int = _lib.SV_MONTGOMERY, out: torch.Tensor = None) -> torch.Tensor:
+    """Batched MSMs over HBM-resident arrays (offsets: (count + 1,) int64 on the device);
+    returns (count, 8) int64 affine results in `form`."""
+    count = offsets.shape[0] - 1
+    if out is None:
+        out = torch.empty((max(count, 1), 8), dtype=torch.int64, device=bases.device)
+    d = _dev_index(bases)
+    _lib.check(_lib.lib.sv_bn254_g1_msm_batch_device(bases.data_ptr(), scalars.data_ptr(), offsets.data_ptr(),
+                                                     count, max_terms, form, d, _stream_handle(bases.device),
+                                                     out.data_ptr()),
+               "sv_bn254_g1_msm_batch_device")
+    return out[:count]

@@ -7,6 +7,10 @@
 * ``multi_scalar_multiplication(scalars, bases)`` mirrors ``util::msm::multi_scalar_multiplication``
   (snark-verifier/src/util/msm.rs:287-316), whose length check is ``assert_eq!`` (msm.rs:288).
 
+* ``batch_multi_scalar_multiplication(msms)`` / ``NativeLoader.multi_scalar_multiplication_batch``
+  evaluate many such MSMs in one call (SURVEY.md 8f1: the per-proof Msm::evaluate calls of a
+  native verifier, bdfg21.rs:75-78 / gwc19.rs:76-79, and accumulation.rs:177-192's pair).
+
 Points are ``(x, y)`` tuples of canonical ints, ``None`` is the identity (halo2curves (0, 0)).
 """
 from __future__ import annotations
@@ -47,6 +51,43 @@ def multi_scalar_multiplication(scalars: Sequence[int], bases: Sequence[Point], 
     return msm_arrays(enc.bases_array(bases), enc.scalars_array(scalars), _lib.SV_CANONICAL, num_gpus)
 
 
+def msm_batch_arrays(bases: np.ndarray, scalars: np.ndarray, offsets: Sequence[int],
+                     form: int = _lib.SV_CANONICAL) -> list:
+    """len(offsets) - 1 MSMs over shared C-ABI host arrays; MSM k uses rows offsets[k]:offsets[k+1]."""
+    bases = np.ascontiguousarray(bases, dtype=np.uint64)
+    scalars = np.ascontiguousarray(scalars, dtype=np.uint64)
+    if bases.shape[0] != scalars.shape[0]:
+        raise ReferencePanic("assertion failed: scalars.len() == bases.len()")
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    count = off.shape[0] - 1
+    if count <= 0:
+        return []
+    if int(off[-1]) > bases.shape[0]:
+        raise _lib.LengthError("msm_batch: offsets run past the arrays")
+    out = (_lib.sv_g1_affine * count)()
+    rc = _lib.lib.sv_bn254_g1_msm_batch(bases.ctypes.data, scalars.ctypes.data, off.ctypes.data, count, form,
+                                        ctypes.cast(out, ctypes.c_void_p))
+    if rc == _lib.SV_ERR_EMPTY:
+        raise ReferencePanic("pairs should not be empty")
+    _lib.check(rc, "sv_bn254_g1_msm_batch")
+    return [enc.g1_from_struct(o, form) for o in out]
+
+
+def batch_multi_scalar_multiplication(msms: Sequence[Sequence[Tuple[int, Point]]]) -> list:
+    """[NativeLoader.multi_scalar_multiplication(pairs) for pairs in msms], one GPU launch."""
+    offsets = [0]
+    scalars, bases = [], []
+    for pairs in msms:
+        if len(pairs) == 0:
+            raise ReferencePanic("pairs should not be empty")
+        scalars += [s for s, _ in pairs]
+        bases += [b for _, b in pairs]
+        offsets.append(len(scalars))
+    if not msms:
+        return []
+    return msm_batch_arrays(enc.bases_array(bases), enc.scalars_array(scalars), offsets)
+
+
 class NativeLoader:
     """Mirror of snark_verifier::loader::native::NativeLoader (stateless, like the reference's
     ``lazy_static`` LOADER, native.rs:11-19)."""
@@ -58,6 +99,10 @@ class NativeLoader:
         scalars = [s for s, _ in pairs]
         bases = [b for _, b in pairs]
         return multi_scalar_multiplication(scalars, bases, num_gpus)
+
+    @staticmethod
+    def multi_scalar_multiplication_batch(msms: Sequence[Sequence[Tuple[int, Point]]]) -> list:
+        return batch_multi_scalar_multiplication(msms)
 
 
 def fold_partials(partials: Sequence[Tuple[int, int, int]], out_form: int = _lib.SV_CANONICAL) -> Point:

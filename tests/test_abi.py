@@ -97,3 +97,20 @@ def test_poseidon_arguments_rejected_without_compute():
     with pytest.raises(_lib.LengthError):
         gp.permute([[1, 2]], 3)
     assert gp.permute([], 3) == [] and gp.squeeze_many([]) == []
+
+
+def test_msm_batch_arguments_rejected_without_compute():
+    import svgpu
+    from svgpu import _lib
+    buf = np.zeros(64, np.uint64)
+    out = np.zeros(64, np.uint64)
+    bad = np.array([0, 2, 1], np.uint64)
+    assert _lib.lib.sv_bn254_g1_msm_batch(buf.ctypes.data, buf.ctypes.data, bad.ctypes.data, 2, 0,
+                                          out.ctypes.data) == _lib.SV_ERR_ARG
+    empty = np.array([0, 1, 1], np.uint64)
+    assert _lib.lib.sv_bn254_g1_msm_batch(buf.ctypes.data, buf.ctypes.data, empty.ctypes.data, 2, 0,
+                                          out.ctypes.data) == _lib.SV_ERR_EMPTY
+    assert _lib.lib.sv_bn254_g1_msm_batch(None, None, None, 0, 0, None) == _lib.SV_OK
+    with pytest.raises(svgpu.ReferencePanic, match="pairs should not be empty"):
+        svgpu.batch_multi_scalar_multiplication([[(1, b.G1_GEN)], []])
+    assert svgpu.batch_multi_scalar_multiplication([]) == []

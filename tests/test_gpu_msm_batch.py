@@ -1,0 +1,110 @@
+"""Batched small MSMs through the C ABI against the C++ oracle (msm.rs
+restatement): ragged sizes, both windows, both forms, the reference's edge suite per MSM,
+big-MSM routing, empty-MSM panic, and the config-5 shape (2 x 64 terms) on device buffers."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import bn254 as b
+
+pytestmark = pytest.mark.gpu
+
+
+def _expected(oracle_cpp, B, S, offsets):
+    return [b.g1_from_bytes(oracle_cpp.msm_pippenger(B[lo:hi], S[lo:hi], 1).tobytes())
+            for lo, hi in zip(offsets[:-1], offsets[1:])]
+
+
+def _ragged(oracle_cpp, sizes, seed):
+    n = sum(sizes)
+    B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=seed)
+    S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=seed)
+    offsets = [0]
+    for m in sizes:
+        offsets.append(offsets[-1] + m)
+    return B, S, offsets
+
+
+@pytest.mark.parametrize("window", ["5", "8"])
+def test_ragged_batch_both_windows(gpu, oracle_cpp, monkeypatch, window):
+    import svgpu
+    monkeypatch.setenv("SVGPU_BATCH_WINDOW_BITS", window)
+    sizes = [1, 2, 3, 63, 64, 65, 127, 128, 129, 200, 255, 256, 257, 300, 513, 1023]
+    B, S, off = _ragged(oracle_cpp, sizes, 1000)
+    assert svgpu.msm_batch_arrays(B, S, off) == _expected(oracle_cpp, B, S, off)
+
+
+def test_montgomery_form(gpu, oracle_cpp, monkeypatch):
+    import svgpu
+    monkeypatch.setenv("SVGPU_BATCH_SEQ_MAX", "0")
+    from svgpu import encoding as enc
+    sizes = [5, 64, 17]
+    B, S, off = _ragged(oracle_cpp, sizes, 77)
+    exp = _expected(oracle_cpp, B, S, off)
+    pts = [enc.g1_from_limbs(r) for r in B]
+    sc = [enc.limbs_to_int(r) for r in S]
+    Bm, Sm = enc.bases_array(pts, svgpu.SV_MONTGOMERY), enc.scalars_array(sc, svgpu.SV_MONTGOMERY)
+    got = svgpu.msm_batch_arrays(Bm, Sm, off, svgpu.SV_MONTGOMERY)
+    assert got == exp
+
+
+def test_edge_suite_per_msm(gpu):
+    """zero scalars, identity bases, P and -P, repeated base, r - 1, 2^k, all-equal scalars."""
+    import svgpu
+    P = b.g1_mul(b.G1_GEN, 987654321)
+    Q = b.g1_mul(b.G1_GEN, 5)
+    msms = [
+        [(0, P), (0, Q)],                                   # -> identity
+        [(3, None), (4, P)],                                # identity base
+        [(7, P), (7, b.g1_neg(P))],                         # cancels
+        [(11, P)] * 40,                                     # repeated base, same scalar
+        [(b.R - 1, P), (1, P)],                             # (r-1)P + P = O
+        [(1 << k, Q) for k in range(0, 254, 7)],            # powers of two
+        [(b.R - 1, Q)] * 70,                                # all-equal, top digits
+        [(random.Random(3).randrange(b.R), P) for _ in range(33)],
+    ]
+    got = svgpu.batch_multi_scalar_multiplication(msms)
+    for pairs, g in zip(msms, got):
+        assert g == b.native_msm([s for s, _ in pairs], [p for _, p in pairs])
+
+
+def test_big_msms_route_to_single_pipeline(gpu, oracle_cpp, monkeypatch):
+    import svgpu
+    monkeypatch.setenv("SVGPU_BATCH_MAX", "100")
+    monkeypatch.setenv("SVGPU_BATCH_SEQ_MAX", "0")
+    sizes = [10, 3000, 50, 101]
+    B, S, off = _ragged(oracle_cpp, sizes, 5000)
+    assert svgpu.msm_batch_arrays(B, S, off) == _expected(oracle_cpp, B, S, off)
+
+
+def test_tiny_batch_sequential_route(gpu, oracle_cpp):
+    import svgpu
+    B, S, off = _ragged(oracle_cpp, [64, 64], 9000)  # config-5 shape: two 64-term MSMs
+    assert svgpu.msm_batch_arrays(B, S, off) == _expected(oracle_cpp, B, S, off)
+
+
+def test_empty_msm_panics(gpu):
+    import svgpu
+    with pytest.raises(svgpu.ReferencePanic, match="pairs should not be empty"):
+        svgpu.batch_multi_scalar_multiplication([[(1, b.G1_GEN)], []])
+
+
+def test_device_api_config5_shape(gpu, oracle_cpp):
+    """64 accumulators -> lhs/rhs MSMs of 64 terms each with [1, r, .., r^63] (accumulation.rs:177-192),
+    plus 126 more 64-term MSMs so the batch holds 128 MSMs (a 64-proof aggregation's per-proof pair)."""
+    import svgpu
+    from svgpu import device as dv
+    count, m = 128, 64
+    n = count * m
+    Bd = dv.gen_bases(dv.empty_bases(n, gpu), b.SEED_BASES, 0, svgpu.SV_MONTGOMERY)
+    Sd = dv.gen_scalars(dv.empty_scalars(n, gpu), b.SEED_SCALARS, 0, svgpu.SV_MONTGOMERY)
+    off = torch.arange(0, n + 1, m, dtype=torch.int64, device=gpu)
+    out = dv.msm_batch(Bd, Sd, off, m, svgpu.SV_MONTGOMERY)
+    torch.cuda.synchronize()
+    from svgpu import encoding as enc
+    got = [enc.g1_from_limbs(r, svgpu.SV_MONTGOMERY) for r in out.cpu().numpy().view(np.uint64)]
+    B = oracle_cpp.gen_bases(b.SEED_BASES, n)
+    S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n)
+    assert got == _expected(oracle_cpp, B, S, list(range(0, n + 1, m)))

@@ -140,6 +140,38 @@ int sv_bn254_poseidon_squeeze_device(sv_fe* d_states, const sv_fe* d_elements,
                                      const uint64_t* d_offsets, size_t n, int t, int form,
                                      sv_fe* d_out, int device, void* stream) SV_NOEXCEPT;
 
+/* ---- codecs around the path, decoded on the device --------
+ * Point encodings:
+ *   SV_ENC_HALO2_COMPRESSED  32 B: x little-endian, parity of y in bit 255, identity = zeros
+ *                            (halo2curves GroupEncoding, read by PoseidonTranscript::read_ec_point,
+ *                            system/halo2/transcript/halo2.rs:247-260)
+ *   SV_ENC_EVM               64 B: x || y big-endian, identity = zeros
+ *                            (EvmTranscript::read_ec_point, system/halo2/transcript/evm.rs:223-242)
+ * g1_decode: n encoded points -> affine in `form`.  All valid: SV_OK and *first_invalid = -1.
+ *   Otherwise SV_ERR_ARG ("Invalid elliptic curve point encoding in proof"), *first_invalid =
+ *   the lowest invalid index, and invalid points are written as (0, 0).
+ * accumulators_from_limbs: LimbsEncoding<LIMBS, BITS>::from_repr (pcs/kzg/accumulator.rs:57-77)
+ *   for n accumulators of 4 * n_limbs Fr limbs each (lhs.x, lhs.y, rhs.x, rhs.y; fe_from_limbs,
+ *   util/arithmetic.rs:262-274; the SDK uses LIMBS = 3, BITS = 88).  `form` applies to the limbs
+ *   and the output.  A coordinate >= p or >= 2^256, or a point off the curve (the reference's
+ *   unwrap panics) gives SV_ERR_ARG with *first_invalid = that accumulator.
+ * kzg_decide_eip197: n_checks 0x180-byte ecPairing (EIP-197) inputs as the EVM decider lays them
+ *   out (pcs/kzg/decider.rs:107-127, loader/evm/loader.rs:338-382): lhs, g2, rhs, -s_g2 with G2
+ *   words (x.c1, x.c0, y.c1, y.c0).  All records must carry the same G2 pair (one deciding key).
+ *   *first_fail = first check whose pairing product is not 1 or whose G1 encoding is invalid
+ *   (the precompile would fail either way), -1 if all pass.                             */
+enum { SV_ENC_HALO2_COMPRESSED = 0, SV_ENC_EVM = 1 };
+int sv_bn254_g1_decode(const uint8_t* data, size_t n, int encoding, int form, sv_g1_affine* out,
+                       int64_t* first_invalid) SV_NOEXCEPT;
+int sv_bn254_g1_decode_device(const uint8_t* d_data, size_t n, int encoding, int form, int device,
+                              void* stream, sv_g1_affine* d_out,
+                              int64_t* first_invalid) SV_NOEXCEPT;
+int sv_bn254_kzg_accumulators_from_limbs(const sv_fe* limbs, size_t n, int n_limbs, int bits,
+                                         int form, sv_g1_affine* lhs, sv_g1_affine* rhs,
+                                         int64_t* first_invalid) SV_NOEXCEPT;
+int sv_bn254_kzg_decide_eip197(const uint8_t* input, size_t n_checks, int num_gpus,
+                               int32_t* first_fail) SV_NOEXCEPT;
+
 /* ---- synthetic inputs (SURVEY.md section 8d generator, index-addressable) -------------
  * Fills device buffers with the deterministic SplitMix64 scalars / try-and-increment bases
  * (elements start .. start+n-1) in the requested form.                                   */

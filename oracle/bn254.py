@@ -20,7 +20,10 @@ What it restates (reference = yuliakot/snark-verifier-axiom, read as text):
 * ``accumulate`` -- ``KzgAs::create_proof`` without zk blind
   (snark-verifier/src/pcs/kzg/accumulation.rs:146-195) with powers of r
   starting at 1 (snark-verifier/src/loader.rs:71-78).
-* ``fe_to_limbs``/``fe_from_limbs`` -- snark-verifier/src/util/arithmetic.rs:262-290.
+* ``fe_to_limbs``/``fe_from_limbs`` -- snark-verifier/src/util/arithmetic.rs:262-290;
+  ``accumulator_from_limbs`` -- LimbsEncoding::from_repr (pcs/kzg/accumulator.rs:57-77).
+* point codecs: ``g1_decompress`` (halo2curves compressed, read by transcript/halo2.rs:247-260),
+  ``g1_evm_decode`` (transcript/evm.rs:223-242), ``eip197_input`` (pcs/kzg/decider.rs:107-127).
 
 The field/curve/pairing arithmetic itself lives in the un-vendored dependency
 halo2curves 0.3.1 (axiom-crypto/halo2 @ 98bc83b, Cargo.lock:1820-1823), which
@@ -878,7 +881,115 @@ def fe_to_limbs(x: int, limbs: int = 3, bits: int = 88) -> List[int]:
 
 
 def fe_from_limbs(ls: Sequence[int], bits: int = 88, modulus: int = P) -> int:
-    return sum(l << (bits * i) for i, l in enumerate(ls)) % modulus
+    """arithmetic.rs:262-274: sum limb_i << (bits * i) (limbs read as canonical ints, no range
+    check per limb), then fe_from_big -> from_repr(..).unwrap(): panics when the sum needs more
+    than 32 bytes or is >= the modulus."""
+    big = sum(int(l) << (bits * i) for i, l in enumerate(ls))
+    if big >= 1 << 256 or big >= modulus:
+        raise CodecError("fe_from_big: from_repr(..).unwrap() on a non-canonical value")
+    return big
+
+
+# ----------------------------------------------------------------------------
+# Codecs on either side of the path (SURVEY.md 8f3 / 8f4)
+# ----------------------------------------------------------------------------
+class CodecError(ValueError):
+    pass
+
+
+POINT_MSG = "Invalid elliptic curve point encoding in proof"
+
+
+def accumulator_from_limbs(limbs: Sequence[int], n_limbs: int = 3, bits: int = 88):
+    """LimbsEncoding<LIMBS, BITS>::from_repr on NativeLoader (pcs/kzg/accumulator.rs:57-77):
+    4 * LIMBS Fr limbs -> [lhs_x, lhs_y, rhs_x, rhs_y] via fe_from_limbs, then
+    C::from_xy(x, y).unwrap() (on-curve or the (0, 0) identity)."""
+    if len(limbs) != 4 * n_limbs:
+        raise CodecError("assertion failed: limbs.len() == 4 * LIMBS")
+    xs = [fe_from_limbs(limbs[i * n_limbs:(i + 1) * n_limbs], bits) for i in range(4)]
+    pts = []
+    for x, y in ((xs[0], xs[1]), (xs[2], xs[3])):
+        pt = None if (x == 0 and y == 0) else (x, y)
+        if pt is not None and not g1_on_curve(pt):
+            raise CodecError("C::from_xy(..).unwrap() on a point off the curve")
+        pts.append(pt)
+    return pts[0], pts[1]
+
+
+def g1_compress(pt) -> bytes:
+    """halo2curves 0.3.1 G1 GroupEncoding::to_bytes (external, restated): x little-endian with the
+    parity of y in bit 7 of byte 31; identity = 32 zero bytes.  Parity unpinned (no vectors)."""
+    if pt is None:
+        return b"\0" * 32
+    b = bytearray(int(pt[0]).to_bytes(32, "little"))
+    b[31] |= (pt[1] & 1) << 7
+    return bytes(b)
+
+
+def g1_decompress(data: bytes):
+    """halo2curves 0.3.1 G1 GroupEncoding::from_bytes (read by PoseidonTranscript::read_ec_point,
+    system/halo2/transcript/halo2.rs:247-260): clear the sign bit, x must be canonical; x == 0 with
+    sign 0 is the identity; otherwise y = sqrt(x^3 + 3) (none -> error), negated when its parity
+    differs from the sign bit."""
+    if len(data) != 32:
+        raise CodecError(POINT_MSG)
+    sign = data[31] >> 7
+    x = int.from_bytes(bytes(data[:31]) + bytes([data[31] & 0x7F]), "little")
+    if x >= P:
+        raise CodecError(POINT_MSG)
+    if x == 0 and sign == 0:
+        return None
+    y = sqrt_fp((x * x * x + B) % P)
+    if y is None:
+        raise CodecError(POINT_MSG)
+    if (y & 1) != sign:
+        y = (P - y) % P
+    return (x, y)
+
+
+def g1_evm_encode(pt) -> bytes:
+    """EvmTranscript point encoding: x || y, 32-byte big-endian each (transcript/evm.rs:223-242)."""
+    if pt is None:
+        return b"\0" * 64
+    return int(pt[0]).to_bytes(32, "big") + int(pt[1]).to_bytes(32, "big")
+
+
+def g1_evm_decode(data: bytes):
+    """EvmTranscript::read_ec_point (transcript/evm.rs:223-242): both coordinates from_repr
+    (canonical, < p), then C::from_xy (on-curve, or (0, 0) = identity)."""
+    if len(data) != 64:
+        raise CodecError(POINT_MSG)
+    x = int.from_bytes(data[:32], "big")
+    y = int.from_bytes(data[32:], "big")
+    if x >= P or y >= P:
+        raise CodecError(POINT_MSG)
+    if x == 0 and y == 0:
+        return None
+    if not g1_on_curve((x, y)):
+        raise CodecError(POINT_MSG)
+    return (x, y)
+
+
+def _g2_words(q) -> bytes:
+    (x0, x1), (y0, y1) = q
+    return b"".join(int(v).to_bytes(32, "big") for v in (x1, x0, y1, y0))
+
+
+def eip197_input(g2, s_g2, lhs, rhs) -> bytes:
+    """The 0x180-byte ecPairing (EIP-197) input the EVM decider builds (pcs/kzg/decider.rs:
+    107-127, loader/evm/loader.rs:338-382): lhs, g2, rhs, -s_g2; G2 words (x.c1, x.c0, y.c1, y.c0)."""
+    return g1_evm_encode(lhs) + _g2_words(g2) + g1_evm_encode(rhs) + _g2_words(g2_neg(s_g2))
+
+
+def eip197_parse(data: bytes):
+    """Inverse of eip197_input: (lhs, g2, rhs, minus_s_g2)."""
+    if len(data) != 0x180:
+        raise CodecError("EIP-197 input must be 0x180 bytes per pairing check")
+
+    def g2_at(o):
+        w = [int.from_bytes(data[o + 32 * i:o + 32 * (i + 1)], "big") for i in range(4)]
+        return ((w[1], w[0]), (w[3], w[2]))
+    return g1_evm_decode(data[0:64]), g2_at(64), g1_evm_decode(data[192:256]), g2_at(256)
 
 
 # ----------------------------------------------------------------------------

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../include/svgpu.h"
+#include "codec.hpp"
 #include "decider.hpp"
 #include "gen.hpp"
 #include "host_ec.hpp"
@@ -470,6 +471,150 @@ int sv_bn254_poseidon_squeeze_device(sv_fe* d_states, const sv_fe* d_elements, c
   if (resolve_gpus(0) == 0) return SV_ERR_DEVICE;
   SV_HIP(hipSetDevice(device));
   return poseidon_squeeze_device(d_states, d_elements, d_offsets, n, t, form, d_out, (hipStream_t)stream);
+  SV_GUARD_END
+}
+
+int sv_bn254_g1_decode(const uint8_t* data, size_t n, int encoding, int form, sv_g1_affine* out,
+                       int64_t* first_invalid) noexcept {
+  SV_GUARD_BEGIN
+  SV_TRY(check_form(form));
+  if (encoding != SV_ENC_HALO2_COMPRESSED && encoding != SV_ENC_EVM) {
+    sv::set_error("unknown point encoding %d", encoding);
+    return SV_ERR_ARG;
+  }
+  int64_t fi = -1;
+  if (first_invalid) *first_invalid = -1;
+  if (n == 0) return SV_OK;
+  if (!data || !out) return SV_ERR_ARG;
+  if (resolve_gpus(1) == 0) return SV_ERR_DEVICE;
+  const int dev = runtime_device_id(0);
+  const size_t rec = encoding == SV_ENC_EVM ? 64 : 32;
+  DevBuf din, dout;
+  SV_TRY(din.alloc(dev, n * rec));
+  SV_TRY(dout.alloc(dev, n * sizeof(sv_g1_affine)));
+  SV_HIP(hipMemcpy(din.p, data, n * rec, hipMemcpyHostToDevice));
+  SV_TRY(g1_decode_device(din.p, n, encoding, rec, 0, form, dev, nullptr, dout.p, &fi));
+  SV_HIP(hipMemcpy(out, dout.p, n * sizeof(sv_g1_affine), hipMemcpyDeviceToHost));
+  if (first_invalid) *first_invalid = fi;
+  if (fi >= 0) {
+    sv::set_error("Invalid elliptic curve point encoding in proof (point %lld)", (long long)fi);
+    return SV_ERR_ARG;
+  }
+  return SV_OK;
+  SV_GUARD_END
+}
+
+int sv_bn254_g1_decode_device(const uint8_t* d_data, size_t n, int encoding, int form, int device, void* stream,
+                              sv_g1_affine* d_out, int64_t* first_invalid) noexcept {
+  SV_GUARD_BEGIN
+  SV_TRY(check_form(form));
+  if (resolve_gpus(0) == 0) return SV_ERR_DEVICE;
+  SV_HIP(hipSetDevice(device));
+  int64_t fi = -1;
+  SV_TRY(g1_decode_device(d_data, n, encoding, encoding == SV_ENC_EVM ? 64 : 32, 0, form, device,
+                          (hipStream_t)stream, d_out, &fi));
+  if (first_invalid) *first_invalid = fi;
+  if (fi >= 0) {
+    sv::set_error("Invalid elliptic curve point encoding in proof (point %lld)", (long long)fi);
+    return SV_ERR_ARG;
+  }
+  return SV_OK;
+  SV_GUARD_END
+}
+
+int sv_bn254_kzg_accumulators_from_limbs(const sv_fe* limbs, size_t n, int n_limbs, int bits, int form,
+                                         sv_g1_affine* lhs, sv_g1_affine* rhs, int64_t* first_invalid) noexcept {
+  SV_GUARD_BEGIN
+  SV_TRY(check_form(form));
+  if (first_invalid) *first_invalid = -1;
+  if (n == 0) return SV_OK;
+  if (!limbs || !lhs || !rhs || n_limbs < 1) return SV_ERR_ARG;
+  if (resolve_gpus(1) == 0) return SV_ERR_DEVICE;
+  const int dev = runtime_device_id(0);
+  const size_t nl = n * 4 * (size_t)n_limbs;
+  DevBuf dl, dlhs, drhs;
+  SV_TRY(dl.alloc(dev, nl * sizeof(sv_fe)));
+  SV_TRY(dlhs.alloc(dev, n * sizeof(sv_g1_affine)));
+  SV_TRY(drhs.alloc(dev, n * sizeof(sv_g1_affine)));
+  SV_HIP(hipMemcpy(dl.p, limbs, nl * sizeof(sv_fe), hipMemcpyHostToDevice));
+  int64_t fi = -1;
+  SV_TRY(limbs_to_accumulators_device(dl.p, n, n_limbs, bits, form, dev, nullptr, dlhs.p, drhs.p, &fi));
+  SV_HIP(hipMemcpy(lhs, dlhs.p, n * sizeof(sv_g1_affine), hipMemcpyDeviceToHost));
+  SV_HIP(hipMemcpy(rhs, drhs.p, n * sizeof(sv_g1_affine), hipMemcpyDeviceToHost));
+  if (first_invalid) *first_invalid = fi;
+  if (fi >= 0) {
+    sv::set_error("accumulator %lld: limbs do not encode a canonical on-curve point", (long long)fi);
+    return SV_ERR_ARG;
+  }
+  return SV_OK;
+  SV_GUARD_END
+}
+
+namespace {
+// 32-byte big-endian word -> canonical limbs; false when >= p
+bool be_word(const uint8_t* w, F& out) {
+  for (int k = 0; k < 4; k++) {
+    uint64_t v = 0;
+    for (int b = 0; b < 8; b++) v = (v << 8) | w[(3 - k) * 8 + b];
+    out.l[k] = v;
+  }
+  return host::f_is_reduced(out);
+}
+bool g2_from_eip197(const uint8_t* r, sv_g2_affine* q) {
+  F w[4];
+  for (int i = 0; i < 4; i++)
+    if (!be_word(r + 32 * i, w[i])) return false;
+  q->x.c1 = fe_out(w[0]);
+  q->x.c0 = fe_out(w[1]);
+  q->y.c1 = fe_out(w[2]);
+  q->y.c0 = fe_out(w[3]);
+  return true;
+}
+}  // namespace
+
+int sv_bn254_kzg_decide_eip197(const uint8_t* input, size_t n_checks, int num_gpus, int32_t* first_fail) noexcept {
+  SV_GUARD_BEGIN
+  (void)num_gpus;  // one device: the records are host memory and the check count is small
+  if (n_checks == 0) {
+    sv::set_error("accumulators should not be empty");
+    return SV_ERR_EMPTY;
+  }
+  if (!input || !first_fail) return SV_ERR_ARG;
+  constexpr size_t kRec = 0x180;
+  sv_g2_affine g2, msg2;
+  if (!g2_from_eip197(input + 64, &g2) || !g2_from_eip197(input + 256, &msg2)) {
+    sv::set_error("EIP-197 record 0: G2 word >= p");
+    return SV_ERR_ARG;
+  }
+  for (size_t i = 1; i < n_checks; i++)
+    if (memcmp(input + i * kRec + 64, input + 64, 128) || memcmp(input + i * kRec + 256, input + 256, 128)) {
+      sv::set_error("EIP-197 record %zu: G2 points differ from record 0 (one deciding key per call)", i);
+      return SV_ERR_ARG;
+    }
+  // s_g2 = -(-s_g2): negate y (canonical)
+  sv_g2_affine sg2 = msg2;
+  {
+    F y0 = fe_in(msg2.y.c0), y1 = fe_in(msg2.y.c1);
+    sg2.y.c0 = fe_out(host::f_sub(F{}, y0));
+    sg2.y.c1 = fe_out(host::f_sub(F{}, y1));
+  }
+  if (resolve_gpus(1) == 0) return SV_ERR_DEVICE;
+  const int dev = runtime_device_id(0);
+  DevBuf din, dl, dr;
+  SV_TRY(din.alloc(dev, n_checks * kRec));
+  SV_TRY(dl.alloc(dev, n_checks * sizeof(sv_g1_affine)));
+  SV_TRY(dr.alloc(dev, n_checks * sizeof(sv_g1_affine)));
+  SV_HIP(hipMemcpy(din.p, input, n_checks * kRec, hipMemcpyHostToDevice));
+  int64_t bl = -1, br = -1;
+  SV_TRY(g1_decode_device(din.p, n_checks, SV_ENC_EVM, kRec, 0, SV_CANONICAL, dev, nullptr, dl.p, &bl));
+  SV_TRY(g1_decode_device(din.p, n_checks, SV_ENC_EVM, kRec, 192, SV_CANONICAL, dev, nullptr, dr.p, &br));
+  int32_t ff = -1;
+  SV_TRY(decide_run_device(&g2, &sg2, dl.p, dr.p, n_checks, SV_CANONICAL, dev, nullptr, &ff, nullptr, nullptr));
+  int64_t first = -1;
+  for (int64_t c : {(int64_t)ff, bl, br})
+    if (c >= 0 && (first < 0 || c < first)) first = c;
+  *first_fail = (int32_t)first;
+  return SV_OK;
   SV_GUARD_END
 }
 

@@ -18,6 +18,9 @@ SV_MONTGOMERY = 1
 
 SV_OK, SV_ERR_EMPTY, SV_ERR_LEN, SV_ERR_ARG, SV_ERR_DEVICE, SV_ERR_OOM = range(6)
 
+SV_ENC_HALO2_COMPRESSED = 0
+SV_ENC_EVM = 1
+
 
 class SvError(RuntimeError):
     status = -1
@@ -102,6 +105,12 @@ PROTOTYPES = [
     ("sv_bn254_poseidon_squeeze", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p]),
     ("sv_bn254_poseidon_squeeze_device", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p,
                                                   c_int, c_void_p]),
+    ("sv_bn254_g1_decode", c_int, [c_void_p, c_size_t, c_int, c_int, c_void_p, POINTER(ctypes.c_int64)]),
+    ("sv_bn254_g1_decode_device", c_int, [c_void_p, c_size_t, c_int, c_int, c_int, c_void_p, c_void_p,
+                                           POINTER(ctypes.c_int64)]),
+    ("sv_bn254_kzg_accumulators_from_limbs", c_int, [c_void_p, c_size_t, c_int, c_int, c_int, c_void_p, c_void_p,
+                                                      POINTER(ctypes.c_int64)]),
+    ("sv_bn254_kzg_decide_eip197", c_int, [c_void_p, c_size_t, c_int, POINTER(c_int32)]),
     ("sv_gen_scalars_device", c_int, [c_void_p, c_size_t, c_uint64, c_uint64, c_int, c_int, c_void_p]),
     ("sv_gen_bases_device", c_int, [c_void_p, c_size_t, c_uint64, c_uint64, c_int, c_int, c_void_p]),
     ("sv_msm_last_stats", c_int, [POINTER(sv_msm_stats)]),

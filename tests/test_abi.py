@@ -114,3 +114,19 @@ def test_msm_batch_arguments_rejected_without_compute():
     with pytest.raises(svgpu.ReferencePanic, match="pairs should not be empty"):
         svgpu.batch_multi_scalar_multiplication([[(1, b.G1_GEN)], []])
     assert svgpu.batch_multi_scalar_multiplication([]) == []
+
+
+def test_codec_arguments_rejected_without_compute():
+    from svgpu import _lib
+    buf = np.zeros(64, np.uint8)
+    out = np.zeros(16, np.uint64)
+    bad = ctypes.c_int64(5)
+    assert _lib.lib.sv_bn254_g1_decode(buf.ctypes.data, 1, 7, 0, out.ctypes.data, ctypes.byref(bad)) == _lib.SV_ERR_ARG
+    assert _lib.lib.sv_bn254_g1_decode(buf.ctypes.data, 0, 0, 0, out.ctypes.data, ctypes.byref(bad)) == _lib.SV_OK
+    assert bad.value == -1
+    ff = ctypes.c_int32(0)
+    assert _lib.lib.sv_bn254_kzg_decide_eip197(buf.ctypes.data, 0, 0, ctypes.byref(ff)) == _lib.SV_ERR_EMPTY
+    recs = np.zeros(2 * 0x180, np.uint8)
+    recs[0x180 + 64] = 1  # record 1 carries a different G2 than record 0
+    assert _lib.lib.sv_bn254_kzg_decide_eip197(recs.ctypes.data, 2, 0, ctypes.byref(ff)) == _lib.SV_ERR_ARG
+    assert "differ" in _lib.last_error()

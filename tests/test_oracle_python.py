@@ -127,3 +127,29 @@ def test_poseidon_sponge_restatement_structure():
     a.update([3])
     c.update([3 + poseidon.FR_MODULUS])
     assert a.squeeze() == c.squeeze()
+
+
+def test_codec_restatements_round_trip():
+    pts = [b.g1_mul(b.G1_GEN, k) for k in (1, 2, 3, 12345, b.R - 1)] + [None]
+    for p in pts:
+        assert b.g1_decompress(b.g1_compress(p)) == p
+        assert b.g1_evm_decode(b.g1_evm_encode(p)) == p
+    with pytest.raises(b.CodecError):
+        b.g1_evm_decode(b.P.to_bytes(32, "big") + (2).to_bytes(32, "big"))   # x >= p
+    with pytest.raises(b.CodecError):
+        b.g1_evm_decode((1).to_bytes(32, "big") + (3).to_bytes(32, "big"))   # off curve
+    bad_x = next(x for x in range(1, 100) if b.sqrt_fp((x ** 3 + 3) % b.P) is None)
+    with pytest.raises(b.CodecError):
+        b.g1_decompress(bad_x.to_bytes(32, "little"))                        # no square root
+    # limbs: SDK LIMBS = 3, BITS = 88
+    lhs, rhs = b.g1_mul(b.G1_GEN, 77), b.g1_mul(b.G1_GEN, 99)
+    limbs = sum((b.fe_to_limbs(c) for c in (lhs[0], lhs[1], rhs[0], rhs[1])), [])
+    assert b.accumulator_from_limbs(limbs) == (lhs, rhs)
+    with pytest.raises(b.CodecError):
+        b.accumulator_from_limbs(limbs[:-1] + [limbs[-1] + 1])              # off curve
+    with pytest.raises(b.CodecError):
+        b.fe_from_limbs([0, 0, 1 << 100])                                    # > 2^256
+    g2, sg2, accs = b.gen_decider_case(2)
+    rec = b.eip197_input(g2, sg2, *accs[0])
+    lhs2, g2p, rhs2, msg2 = b.eip197_parse(rec)
+    assert (lhs2, g2p, rhs2, msg2) == (accs[0][0], g2, accs[0][1], b.g2_neg(sg2))

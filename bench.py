@@ -45,12 +45,57 @@ def parse():
     ap.add_argument("--log-n", type=int, default=20, help="points per GPU = 2^log_n")
     ap.add_argument("--decider-n", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the batch-MSM / config-5 / Poseidon lines")
     return ap.parse_args()
 
 
 def ref_window(n: int) -> int:
     import math
     return int(math.ceil(math.log(n))) + 2
+
+
+def _time(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps, r
+
+
+def next_rows(dev, dv, ob, enc, g2, sg2, accs):
+    import svgpu
+    M = svgpu.SV_MONTGOMERY
+    res = {}
+    # f1: 128 MSMs x 64 terms (the per-proof pair of a 64-proof aggregation) in one launch
+    count, m = 128, 64
+    B = dv.gen_bases(dv.empty_bases(count * m, dev), ob.SEED_BASES, 0, M)
+    S = dv.gen_scalars(dv.empty_scalars(count * m, dev), ob.SEED_SCALARS, 0, M)
+    off = torch.arange(0, count * m + 1, m, dtype=torch.int64, device=dev)
+    t, _ = _time(lambda: dv.msm_batch(B, S, off, m, M), 5)
+    res["msm_batch"] = {"msms": count, "terms_each": m, "ms": t * 1e3, "terms_per_s": count * m / t}
+    # config 5: 64 valid accumulators -> KzgAs::create_proof MSMs (r^0..r^63) -> one decide
+    acc64 = accs[:64]
+    r = ob.gen_scalar(ob.SEED_SCALARS, 1 << 30)
+    inst = [svgpu.KzgAccumulator(a[0], a[1]) for a in acc64]
+    dk = svgpu.KzgDecidingKey(ob.G1_GEN, g2, sg2)
+
+    def aggregate():
+        acc = svgpu.KzgAs.create_proof(inst, r)
+        svgpu.KzgAs.decide(dk, acc)
+        return acc
+    t, acc = _time(aggregate, 5)
+    exp = ob.accumulate(acc64, r)
+    res["config5_aggregation"] = {"accumulators": 64, "latency_ms": t * 1e3, "verdict": "pass",
+                                  "parity_vs_oracle": bool((acc.lhs, acc.rhs) == exp)}
+    # f2: batched Poseidon permutations (t = 3, the SDK transcript's width), HBM-resident states
+    n = 1 << 20
+    st = torch.randint(0, 1 << 62, (n * 3, 4), dtype=torch.int64, device=dev)
+    st[:, 3] &= (1 << 59) - 1
+    t, _ = _time(lambda: dv.poseidon_permute(st, 3, M), 5)
+    res["poseidon"] = {"width": 3, "states": n, "ms": t * 1e3, "permutations_per_s": n / t}
+    return res
 
 
 def main():
@@ -134,6 +179,12 @@ def main():
     dec_s = float(dt.item())
     pairings_per_s = 2 * dn * world * dsteps / dec_s
 
+    # ---- "next" rows, rank 0 only: batched small MSMs, config-5 aggregation
+    #      latency (accumulate 64 accumulators with r^i, then decide), batched Poseidon permutations
+    extra = {}
+    if rank == 0 and not args.no_extras:
+        extra = next_rows(dev, dv, ob, enc, g2, sg2, accs)
+
     # ---- roofline of the dominant kernel (k_accumulate), timed with HIP events on its stream
     acc_avg_ms = float(np.mean(acc_ms))
     entries = stats["entries"]
@@ -205,6 +256,7 @@ def main():
         },
     }
 
+    out.update(extra)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import cpu_ref
         threads = min(16, os.cpu_count() or 1)

@@ -16,7 +16,8 @@ os.makedirs(dst, exist_ok=True)
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "").replace("sv::", "")
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "").replace("sv::", "")
+    return name.split("(")[0]
 
 
 rows = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
@@ -26,6 +27,13 @@ lines = [f"# rocprofv3 --kernel-trace --stats, bench.py --steps 10 --warmup 2 ({
 for r in rows:
     lines.append("| %s | %s | %.1f | %.3f | %.1f |" % (short(r["Name"]), r["Calls"], float(r["AverageNs"]) / 1e3,
                                                        float(r["TotalDurationNs"]) / 1e6, float(r["Percentage"])))
+ex = os.path.join(src, "trace_extras", "run_kernel_stats.csv")
+if os.path.exists(ex):
+    lines += ["", "## bench.py with the next-row extras (batched MSMs, config-5 aggregation, Poseidon)", "",
+              "| kernel | calls | avg us | total ms | % |", "|---|---|---|---|---|"]
+    for r in csv.DictReader(open(ex)):
+        lines.append("| %s | %s | %.1f | %.3f | %.1f |" % (short(r["Name"]), r["Calls"], float(r["AverageNs"]) / 1e3,
+                                                           float(r["TotalDurationNs"]) / 1e6, float(r["Percentage"])))
 pmc = {}
 for counter, sub in (("FETCH_SIZE", "pmc_fetch"), ("WRITE_SIZE", "pmc_write")):
     acc = defaultdict(list)

@@ -6,12 +6,13 @@
 //
 // Pipeline (all on one stream, inputs already in HBM):
 //   k_to_mont_bases   (canonical input only) bases -> Montgomery workspace copy
-//   k_digits          scalar -> W signed c-bit digits  dig[w][i] = |d| | sign<<31 (0 = zero digit)
-//   k_hist            per (chunk, window) LDS histogram over the 2^(c-1) buckets -> cnt
-//   k_scan_chunks     per bucket: exclusive prefix over chunks, bucket totals
-//   k_scan_window     per window: exclusive scan of bucket totals (one 1024-thread block)
-//   k_finalize        global bucket offsets gst[], owner bucket of every accumulate chunk
-//   k_scatter         per (chunk, window): LDS cursors, entries sorted by bucket -> ent[]
+//   k_bin_hist        per block of 2048 points: signed c-bit digits of every window (never
+//                     stored), LDS histogram of (window, coarse bin = top bits of the bucket)
+//   k_bin_scan_chunks / k_bin_scan   offsets of every (window, bin, block) run
+//   k_bin_scatter     digits again; entries appended to their block's (window, bin) run -> tmp
+//   k_fine_sort       one block per (window, bin): counting sort by the fine bucket index inside
+//                     the bin's L2-resident region -> ent[], bucket offsets gst[], owner bucket of
+//                     every accumulate chunk tstart[]
 //   k_accumulate      each thread sums K consecutive sorted entries (mixed XYZZ adds; perfect
 //                     load balance whatever the digit distribution), complete buckets written
 //                     directly, bucket pieces that cross a thread boundary to pfirst/plast
@@ -94,20 +95,10 @@ __global__ void k_to_mont_bases(const G1Aff* __restrict__ in, G1Aff* __restrict_
 }
 
 // Signed windows: digit_w = bits[cw, cw+c) + carry, mapped to (-2^(c-1), 2^(c-1)].  W = ceil(255/c)
-// windows so the top digit never carries out (scalars < r < 2^254).
-template <int C>
-__global__ void k_digits(const Fr* __restrict__ scalars, uint32_t n, int mont_in,
-                         uint32_t* __restrict__ dig, uint32_t* __restrict__ err) {
+// windows so the top digit never carries out (scalars < r < 2^254).  f(w, mag, neg) per window.
+template <int C, class F>
+__device__ __forceinline__ void for_each_digit(const Fr& s, F&& f) {
   constexpr int W = (255 + C - 1) / C;
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint4* p = reinterpret_cast<const uint4*>(scalars + i);
-  uint4 q0 = p[0], q1 = p[1];
-  Fr s;
-  s.v[0] = q0.x; s.v[1] = q0.y; s.v[2] = q0.z; s.v[3] = q0.w;
-  s.v[4] = q1.x; s.v[5] = q1.y; s.v[6] = q1.z; s.v[7] = q1.w;
-  if (!s.is_reduced()) atomicOr(err, 2u);
-  if (mont_in) s = fe_from_mont(s);
   uint32_t carry = 0;
   const uint32_t half = 1u << (C - 1);
   const uint32_t mask = (1u << C) - 1;
@@ -115,132 +106,264 @@ __global__ void k_digits(const Fr* __restrict__ scalars, uint32_t n, int mont_in
   for (int w = 0; w < W; w++) {
     const int pos = w * C;
     const int limb = pos >> 5, off = pos & 31;
-    uint32_t lo = limb < 8 ? s.v[limb] : 0;
-    uint32_t hi = (limb + 1) < 8 ? s.v[limb + 1] : 0;
+    const uint32_t lo = limb < 8 ? s.v[limb] : 0;
+    const uint32_t hi = (limb + 1) < 8 ? s.v[limb + 1] : 0;
     uint32_t bits = off ? ((lo >> off) | (hi << (32 - off))) : lo;
     bits = (bits & mask) + carry;
-    uint32_t out;
     if (bits > half) {
       // digit = bits - 2^C <= 0; bits == 2^C (all-ones window + carry) is digit 0 with carry 1
-      const uint32_t mag = (1u << C) - bits;
-      out = mag ? (mag | 0x80000000u) : 0u;
+      f(w, (1u << C) - bits, 1u);
       carry = 1;
     } else {
-      out = bits;
+      f(w, bits, 0u);
       carry = 0;
     }
-    dig[(size_t)w * n + i] = out;
   }
 }
 
-// One block per (chunk, window): LDS histogram of the chunk's digits of this window.
-template <int LOGB>
-__global__ void __launch_bounds__(1024) k_hist(const uint32_t* __restrict__ dig, uint32_t n,
-                                               uint32_t chunk, uint32_t nch,
-                                               uint32_t* __restrict__ cnt) {
-  constexpr uint32_t B = 1u << LOGB;
-  __shared__ uint32_t h[B];
-  const uint32_t ch = blockIdx.x, w = blockIdx.y;
-  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) h[b] = 0;
+__device__ __forceinline__ Fr load_scalar(const Fr* __restrict__ scalars, uint32_t i, int mont_in,
+                                          uint32_t* __restrict__ err) {
+  const uint4* p = reinterpret_cast<const uint4*>(scalars + i);
+  const uint4 q0 = p[0], q1 = p[1];
+  Fr s;
+  s.v[0] = q0.x; s.v[1] = q0.y; s.v[2] = q0.z; s.v[3] = q0.w;
+  s.v[4] = q1.x; s.v[5] = q1.y; s.v[6] = q1.z; s.v[7] = q1.w;
+  if (err && !s.is_reduced()) atomicOr(err, 2u);
+  return mont_in ? fe_from_mont(s) : s;
+}
+
+// ---- two-level counting sort of the n * W (point, digit) entries by bucket ------------------
+// Bucket b = |digit| - 1 of window w splits into a coarse bin b >> FB (NBIN = 2^CB bins per window)
+// and a fine index b & (2^FB - 1).  Pass 1 (k_bin_hist): per block of sort_chunk(c) points, every
+// window's digits, LDS histogram of (window, bin).  Pass 2 (k_bin_scan_chunks, k_bin_scan): global
+// offsets of every (window, bin, block) run.  Pass 3 (k_bin_scatter): the digits again, each
+// entry appended to its block's run -> tmp (u64: fine << 32 | point | sign << 31); a block's runs
+// are short contiguous spans, so writes merge in L2.  Pass 4 (k_fine_sort): one block per
+// (window, bin) counting-sorts its ~n / NBIN entries by fine index inside that bin's region (L2
+// resident), writes ent[], the global bucket offsets gst[] and the owner bucket tstart[t] of every
+// accumulate chunk [tK, tK + K).  No per-(window, point) digit array is ever stored.
+// points per block in passes 1 and 3: 512 (2 per thread), 256 when the LDS staging of W digits
+// per point would not fit (small c, many windows)
+__host__ __device__ constexpr uint32_t sort_chunk(int c) { return (255 + c - 1) / c > 20 ? 256u : 512u; }
+
+// exclusive scan of x[0 .. N) in LDS by a 256-thread block (N <= 4096); returns the total
+template <int N>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t* x, uint32_t* part) {
+  constexpr int PER = (N + kBlock - 1) / kBlock;
+  const int tid = threadIdx.x;
+  uint32_t loc[PER];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < PER; j++) {
+    const int k = tid * PER + j;
+    loc[j] = k < N ? x[k] : 0u;
+    sum += loc[j];
+  }
+  part[tid] = sum;
   __syncthreads();
-  const uint32_t lo = ch * chunk, hi = min(n, lo + chunk);
-  const uint32_t* d = dig + (size_t)w * n;
-  for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    uint32_t v = d[i];
-    if (v) atomicAdd(&h[(v & 0x7fffffffu) - 1], 1u);
+  for (int off = 1; off < kBlock; off <<= 1) {
+    const uint32_t u = tid >= off ? part[tid - off] : 0u;
+    __syncthreads();
+    part[tid] += u;
+    __syncthreads();
+  }
+  uint32_t run = part[tid] - sum;
+  const uint32_t total = part[kBlock - 1];
+#pragma unroll
+  for (int j = 0; j < PER; j++) {
+    const int k = tid * PER + j;
+    if (k < N) x[k] = run;
+    run += loc[j];
   }
   __syncthreads();
-  uint32_t* out = cnt + ((size_t)w * nch + ch) * B;
-  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) out[b] = h[b];
+  return total;
 }
 
-// Per global bucket g = w*B + b: exclusive prefix of cnt over chunks; total -> tot[g].
-__global__ void k_scan_chunks(uint32_t* __restrict__ cnt, uint32_t B, uint32_t W, uint32_t nch,
-                              uint32_t* __restrict__ tot) {
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= B * W) return;
-  uint32_t w = g / B, b = g % B;
-  uint32_t run = 0;
-  for (uint32_t ch = 0; ch < nch; ch++) {
-    size_t k = ((size_t)w * nch + ch) * B + b;
-    uint32_t c = cnt[k];
-    cnt[k] = run;
-    run += c;
+template <int C>
+__global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scalars, uint32_t n, int mont_in,
+                                                     uint32_t nblk, uint32_t* __restrict__ bcnt,
+                                                     uint32_t* __restrict__ err) {
+  constexpr int W = (255 + C - 1) / C, LOGB = C - 1;
+  constexpr int CB = LOGB < 6 ? LOGB : 6, FB = LOGB - CB, NBIN = 1 << CB;
+  __shared__ uint32_t h[W * NBIN];
+  for (int k = threadIdx.x; k < W * NBIN; k += kBlock) h[k] = 0;
+  __syncthreads();
+  constexpr uint32_t CH = sort_chunk(C);
+  const uint32_t lo = blockIdx.x * CH, hi = min(n, lo + CH);
+  for (uint32_t i = lo + threadIdx.x; i < hi; i += kBlock) {
+    const Fr s = load_scalar(scalars, i, mont_in, err);
+    for_each_digit<C>(s, [&](int w, uint32_t mag, uint32_t) {
+      if (mag) atomicAdd(&h[w * NBIN + ((mag - 1) >> FB)], 1u);
+    });
   }
-  tot[g] = run;
+  __syncthreads();
+  // layout bcnt[(w * NBIN + bin) * nblk + blk]: each (window, bin) scans over contiguous blocks
+  for (int k = threadIdx.x; k < W * NBIN; k += kBlock) bcnt[(size_t)k * nblk + blockIdx.x] = h[k];
 }
 
-// One 1024-thread block per window: exclusive scan of tot[w*B .. w*B+B) -> bst, total -> wcnt[w].
-__global__ void __launch_bounds__(1024) k_scan_window(const uint32_t* __restrict__ tot, uint32_t B,
-                                                      uint32_t* __restrict__ bst,
-                                                      uint32_t* __restrict__ wcnt) {
+// one 256-thread block per (window, bin): exclusive scan over blocks in place, total -> btot
+__global__ void __launch_bounds__(kBlock) k_bin_scan_chunks(uint32_t* __restrict__ bcnt, uint32_t nblk,
+                                                            uint32_t* __restrict__ btot) {
+  __shared__ uint32_t part[kBlock];
+  uint32_t* c = bcnt + (size_t)blockIdx.x * nblk;
+  const uint32_t tid = threadIdx.x, per = (nblk + kBlock - 1) / kBlock;
+  const uint32_t lo = min(nblk, tid * per), hi = min(nblk, lo + per);
+  uint32_t sum = 0;
+  for (uint32_t b = lo; b < hi; b++) sum += c[b];
+  part[tid] = sum;
+  __syncthreads();
+  for (uint32_t off = 1; off < kBlock; off <<= 1) {
+    const uint32_t u = tid >= off ? part[tid - off] : 0u;
+    __syncthreads();
+    part[tid] += u;
+    __syncthreads();
+  }
+  uint32_t run = part[tid] - sum;
+  for (uint32_t b = lo; b < hi; b++) {
+    const uint32_t v = c[b];
+    c[b] = run;
+    run += v;
+  }
+  if (tid == kBlock - 1) btot[blockIdx.x] = part[kBlock - 1];
+}
+
+// one 1024-thread block: exclusive scan of btot over all (window, bin) -> bstart; bstart[nwb] = total
+__global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __restrict__ btot, uint32_t nwb,
+                                                   uint32_t* __restrict__ bstart) {
   __shared__ uint32_t part[1024];
-  const uint32_t w = blockIdx.x, tid = threadIdx.x;
-  const uint32_t per = (B + 1023) / 1024;
-  const uint32_t lo = min(B, tid * per), hi = min(B, lo + per);
-  const uint32_t* t = tot + (size_t)w * B;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t per = (nwb + 1023) / 1024;
+  const uint32_t lo = min(nwb, tid * per), hi = min(nwb, lo + per);
   uint32_t s = 0;
-  for (uint32_t b = lo; b < hi; b++) s += t[b];
+  for (uint32_t k = lo; k < hi; k++) s += btot[k];
   part[tid] = s;
   __syncthreads();
   for (uint32_t off = 1; off < 1024; off <<= 1) {
-    uint32_t v = tid >= off ? part[tid - off] : 0;
+    const uint32_t v = tid >= off ? part[tid - off] : 0;
     __syncthreads();
     part[tid] += v;
     __syncthreads();
   }
-  uint32_t run = part[tid] - s;  // exclusive
-  uint32_t* o = bst + (size_t)w * B;
-  for (uint32_t b = lo; b < hi; b++) {
-    o[b] = run;
-    run += t[b];
+  uint32_t run = part[tid] - s;
+  for (uint32_t k = lo; k < hi; k++) {
+    bstart[k] = run;
+    run += btot[k];
   }
-  if (tid == 1023) wcnt[w] = part[1023];
+  if (tid == 1023) bstart[nwb] = part[1023];
 }
 
-// Global offsets gst[g] (windows concatenated), sentinel gst[W*B] = total entries, and the
-// owner bucket tstart[t] of every accumulate chunk [tK, tK+K).
-__global__ void k_finalize(const uint32_t* __restrict__ bst, const uint32_t* __restrict__ tot,
-                           const uint32_t* __restrict__ wcnt, uint32_t B, uint32_t W, uint32_t K,
-                           uint32_t* __restrict__ gst, uint32_t* __restrict__ tstart) {
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g > B * W) return;
-  if (g == B * W) {
-    uint32_t m = 0;
-    for (uint32_t w = 0; w < W; w++) m += wcnt[w];
-    gst[g] = m;
-    return;
-  }
-  uint32_t w = g / B;
-  uint32_t base = 0;
-  for (uint32_t k = 0; k < w; k++) base += wcnt[k];
-  uint32_t s = base + bst[g];
-  uint32_t e = s + tot[g];
-  gst[g] = s;
-  for (uint32_t t = (s + K - 1) / K; t * K < e; t++) tstart[t] = g;
-}
-
-template <int LOGB>
-__global__ void __launch_bounds__(1024) k_scatter(const uint32_t* __restrict__ dig, uint32_t n,
-                                                  uint32_t chunk, uint32_t nch,
-                                                  const uint32_t* __restrict__ cnt,
-                                                  const uint32_t* __restrict__ gst,
-                                                  uint32_t* __restrict__ ent) {
-  constexpr uint32_t B = 1u << LOGB;
-  __shared__ uint32_t cur[B];
-  const uint32_t ch = blockIdx.x, w = blockIdx.y;
-  const uint32_t* c = cnt + ((size_t)w * nch + ch) * B;
-  const uint32_t* g = gst + (size_t)w * B;
-  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) cur[b] = g[b] + c[b];
+// Pass 3: the block's entries are first placed in LDS grouped by (window, bin), then each group
+// is copied to its global run with consecutive lanes writing consecutive addresses.
+template <int C>
+__global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ scalars, uint32_t n, int mont_in,
+                                                        uint32_t nblk, const uint32_t* __restrict__ bcnt,
+                                                        const uint32_t* __restrict__ bstart,
+                                                        uint64_t* __restrict__ tmp) {
+  constexpr int W = (255 + C - 1) / C, LOGB = C - 1;
+  constexpr int CB = LOGB < 6 ? LOGB : 6, FB = LOGB - CB, NBIN = 1 << CB, NK = W * NBIN;
+  constexpr uint32_t FMASK = (1u << FB) - 1;
+  constexpr uint32_t CH = sort_chunk(C), PT = CH / kBlock;
+  __shared__ uint32_t off[NK];   // local group offsets
+  __shared__ uint32_t cur[NK];   // cursors
+  __shared__ uint32_t part[kBlock];
+  __shared__ uint32_t stage[CH * W];  // local point (9 bits) | sign << 9 | fine << 10
+  __shared__ uint16_t key[CH * W];
+  const uint32_t blk = blockIdx.x, lo = blk * CH, hi = min(n, lo + CH);
+  for (int k = threadIdx.x; k < NK; k += kBlock) off[k] = 0;
   __syncthreads();
-  const uint32_t lo = ch * chunk, hi = min(n, lo + chunk);
-  const uint32_t* d = dig + (size_t)w * n;
-  for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    uint32_t v = d[i];
-    if (v) {
-      uint32_t pos = atomicAdd(&cur[(v & 0x7fffffffu) - 1], 1u);
-      ent[pos] = i | (v & 0x80000000u);
+  Fr sc[PT];
+#pragma unroll
+  for (int j = 0; j < (int)PT; j++) {
+    const uint32_t i = lo + threadIdx.x + j * kBlock;
+    if (i < hi) {
+      sc[j] = load_scalar(scalars, i, mont_in, nullptr);
+      for_each_digit<C>(sc[j], [&](int w, uint32_t mag, uint32_t) {
+        if (mag) atomicAdd(&off[w * NBIN + ((mag - 1) >> FB)], 1u);
+      });
     }
+  }
+  __syncthreads();
+  const uint32_t total = block_excl_scan<NK>(off, part);
+  for (int k = threadIdx.x; k < NK; k += kBlock) cur[k] = off[k];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < (int)PT; j++) {
+    const uint32_t li = threadIdx.x + j * kBlock;
+    if (lo + li < hi) {
+      for_each_digit<C>(sc[j], [&](int w, uint32_t mag, uint32_t neg) {
+        if (mag) {
+          const uint32_t b = mag - 1;
+          const uint32_t k = w * NBIN + (b >> FB);
+          const uint32_t pos = atomicAdd(&cur[k], 1u);
+          stage[pos] = li | (neg << 9) | ((b & FMASK) << 10);
+          key[pos] = (uint16_t)k;
+        }
+      });
+    }
+  }
+  __syncthreads();
+  // global position of local slot x = gbase[key] + x  (cur[] reused for gbase)
+  for (int k = threadIdx.x; k < NK; k += kBlock) cur[k] = bstart[k] + bcnt[(size_t)k * nblk + blk] - off[k];
+  __syncthreads();
+  for (uint32_t x = threadIdx.x; x < total; x += kBlock) {
+    const uint32_t e = stage[x];
+    tmp[cur[key[x]] + x] = ((uint64_t)(e >> 10) << 32) | (lo + (e & 511u)) | (((e >> 9) & 1u) << 31);
+  }
+}
+
+// one block per (window, bin): counting sort by the fine index within the bin's region
+__global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__ tmp,
+                                                    const uint32_t* __restrict__ bstart, uint32_t FB, uint32_t K,
+                                                    uint32_t* __restrict__ gst, uint32_t* __restrict__ tstart,
+                                                    uint32_t* __restrict__ ent) {
+  __shared__ uint32_t fc[512];
+  __shared__ uint32_t part[1024];
+  const uint32_t wb = blockIdx.x, tid = threadIdx.x, NF = 1u << FB;
+  const uint32_t s0 = bstart[wb], s1 = bstart[wb + 1];
+  for (uint32_t f = tid; f < NF; f += 1024) fc[f] = 0;
+  __syncthreads();
+  {
+    uint32_t e = s0 + tid;
+    for (; e + 3 * 1024 < s1; e += 4 * 1024) {  // 4 loads in flight per thread
+      const uint32_t f0 = (uint32_t)(tmp[e] >> 32), f1 = (uint32_t)(tmp[e + 1024] >> 32);
+      const uint32_t f2 = (uint32_t)(tmp[e + 2048] >> 32), f3 = (uint32_t)(tmp[e + 3072] >> 32);
+      atomicAdd(&fc[f0], 1u);
+      atomicAdd(&fc[f1], 1u);
+      atomicAdd(&fc[f2], 1u);
+      atomicAdd(&fc[f3], 1u);
+    }
+    for (; e < s1; e += 1024) atomicAdd(&fc[(uint32_t)(tmp[e] >> 32)], 1u);
+  }
+  __syncthreads();
+  // exclusive scan of fc[0 .. NF) (NF <= 512)
+  const uint32_t v = tid < NF ? fc[tid] : 0;
+  part[tid] = v;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    const uint32_t u = tid >= off ? part[tid - off] : 0;
+    __syncthreads();
+    part[tid] += u;
+    __syncthreads();
+  }
+  if (tid < NF) {
+    const uint32_t st = s0 + part[tid] - v, en = st + v;
+    const uint32_t g = wb * NF + tid;  // global bucket = w * B + b
+    gst[g] = st;
+    fc[tid] = st;
+    for (uint32_t t = (st + K - 1) / K; t * K < en; t++) tstart[t] = g;
+  }
+  __syncthreads();
+  uint32_t e = s0 + tid;
+  for (; e + 3 * 1024 < s1; e += 4 * 1024) {
+    uint64_t x[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) x[j] = tmp[e + j * 1024];
+#pragma unroll
+    for (int j = 0; j < 4; j++) ent[atomicAdd(&fc[(uint32_t)(x[j] >> 32)], 1u)] = (uint32_t)x[j];
+  }
+  for (; e < s1; e += 1024) {
+    const uint64_t x = tmp[e];
+    ent[atomicAdd(&fc[(uint32_t)(x >> 32)], 1u)] = (uint32_t)x;
   }
 }
 
@@ -417,14 +540,14 @@ MsmPlan msm_plan(size_t n) {
   uint64_t K = entries / (1u << 18);
   if (K < 4) K = 4;
   if (K > 32) K = 32;
+  // large n: buckets average entries / nbt >> 32 entries; keep a bucket within ~2-3 threads so the
+  // fixup stays a short serial join (a 2^24 MSM at c = 16 has 512 entries per bucket)
+  const uint64_t half_bucket = entries / p.nbt / 2;
+  if (K < half_bucket) K = half_bucket < 512 ? half_bucket : 512;
   if (const char* e = getenv("SVGPU_ACC_K")) K = (uint64_t)atoi(e);
   if (K < 1) K = 1;
   p.K = (uint32_t)K;
   p.T = cdiv(entries, p.K);
-  uint32_t want_ch = cdiv(256, p.W);
-  uint32_t max_ch = cdiv(n, 4096);
-  p.nch = std::max<uint32_t>(1, std::min(want_ch, max_ch));
-  p.chunk = cdiv(n, p.nch);
   // reduction: J running-sum segments per window, NG subset groups of H = J/2 points
   p.J = p.B / kRedL;
   p.logJ = 0;
@@ -508,16 +631,19 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
   const uint64_t entries = (uint64_t)n * p.W;
 
   // ---- workspace layout
+  const int LOGB = p.c - 1;
+  const uint32_t CB = LOGB < 6 ? (uint32_t)LOGB : 6u, FB = (uint32_t)LOGB - CB, NBIN = 1u << CB;
+  const uint32_t nwb = p.W * NBIN;
+  const uint32_t nblk = cdiv(n, sort_chunk(p.c));
   size_t bytes = 0;
   auto add = [&](size_t b) { bytes += Workspace::aligned(b); };
   bool conv = (form == SV_CANONICAL);
   if (conv) add(n * sizeof(G1Aff));
-  add(256);                                   // err flag
-  add(entries * 4);                           // dig
-  add((size_t)p.W * p.nch * p.B * 4);         // cnt
-  add((size_t)p.nbt * 4);                     // tot
-  add((size_t)p.nbt * 4);                     // bst
-  add(64 * 4);                                // wcnt
+  add(256);                                   // err flag + heavy-queue counter
+  add((size_t)nwb * nblk * 4);                // bcnt
+  add((size_t)nwb * 4);                       // btot
+  add(((size_t)nwb + 1) * 4);                 // bstart
+  add(entries * 8);                           // tmp (coarse-binned entries)
   add(((size_t)p.nbt + 1) * 4);               // gst
   add(entries * 4);                           // ent
   add(((size_t)p.T + 1) * 4);                 // tstart
@@ -525,19 +651,20 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
   add((size_t)p.nbt * sizeof(G1Xyzz));        // bsum
   add((size_t)p.nbt * 4);                     // heavy-bucket queue
   const size_t nfinal = (size_t)p.W * p.NG;
-  add((size_t)p.J * p.W * sizeof(G1Xyzz) * 2);         // acc_j, T_j
-  add(nfinal * sizeof(G1Xyzz));                        // group sums
+  add((size_t)p.J * p.W * sizeof(G1Xyzz) * 2);  // acc_j, T_j
+  add(nfinal * sizeof(G1Xyzz));                 // group sums
   SV_TRY(ws->reserve(bytes));
   SV_TRY(ws->reserve_pinned(nfinal * sizeof(G1Xyzz) + 256));
 
   const G1Aff* bases = reinterpret_cast<const G1Aff*>(d_bases);
+  const Fr* scalars = reinterpret_cast<const Fr*>(d_scalars);
+  const int mont_in = form == SV_MONTGOMERY ? 1 : 0;
   G1Aff* bases_m = conv ? ws->carve<G1Aff>(n) : nullptr;
   uint32_t* err = ws->carve<uint32_t>(64);
-  uint32_t* dig = ws->carve<uint32_t>(entries);
-  uint32_t* cnt = ws->carve<uint32_t>((size_t)p.W * p.nch * p.B);
-  uint32_t* tot = ws->carve<uint32_t>(p.nbt);
-  uint32_t* bst = ws->carve<uint32_t>(p.nbt);
-  uint32_t* wcnt = ws->carve<uint32_t>(64);
+  uint32_t* bcnt = ws->carve<uint32_t>((size_t)nwb * nblk);
+  uint32_t* btot = ws->carve<uint32_t>(nwb);
+  uint32_t* bstart = ws->carve<uint32_t>((size_t)nwb + 1);
+  uint64_t* tmp = ws->carve<uint64_t>(entries);
   uint32_t* gst = ws->carve<uint32_t>((size_t)p.nbt + 1);
   uint32_t* ent = ws->carve<uint32_t>(entries);
   uint32_t* tstart = ws->carve<uint32_t>((size_t)p.T + 1);
@@ -558,20 +685,15 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
                        bases, bases_m, (uint32_t)n, err);
     bases = bases_m;
   }
-  SV_LAUNCH_C(k_digits, p.c, dim3(cdiv(n, kBlock)), dim3(kBlock),
-              reinterpret_cast<const Fr*>(d_scalars), (uint32_t)n, form == SV_MONTGOMERY ? 1 : 0,
-              dig, err);
+  SV_LAUNCH_C(k_bin_hist, p.c, dim3(nblk), dim3(kBlock), scalars, (uint32_t)n, mont_in, nblk, bcnt, err);
   SV_HIP(hipGetLastError());
   SV_HIP(hipEventRecord(ev[1], st));
-  const int logb = p.c - 1;
-  SV_LAUNCH_LOGB(k_hist, logb, dim3(p.nch, p.W), dim3(1024), dig, (uint32_t)n, p.chunk, p.nch, cnt);
-  hipLaunchKernelGGL(k_scan_chunks, dim3(cdiv(p.nbt, kBlock)), dim3(kBlock), 0, st, cnt, p.B, p.W,
-                     p.nch, tot);
-  hipLaunchKernelGGL(k_scan_window, dim3(p.W), dim3(1024), 0, st, tot, p.B, bst, wcnt);
-  hipLaunchKernelGGL(k_finalize, dim3(cdiv(p.nbt + 1, kBlock)), dim3(kBlock), 0, st, bst, tot, wcnt,
-                     p.B, p.W, p.K, gst, tstart);
-  SV_LAUNCH_LOGB(k_scatter, logb, dim3(p.nch, p.W), dim3(1024), dig, (uint32_t)n, p.chunk, p.nch, cnt,
-                 gst, ent);
+  hipLaunchKernelGGL(k_bin_scan_chunks, dim3(nwb), dim3(kBlock), 0, st, bcnt, nblk, btot);
+  hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, btot, nwb, bstart);
+  SV_LAUNCH_C(k_bin_scatter, p.c, dim3(nblk), dim3(kBlock), scalars, (uint32_t)n, mont_in, nblk, bcnt, bstart,
+              tmp);
+  hipLaunchKernelGGL(k_fine_sort, dim3(nwb), dim3(1024), 0, st, tmp, bstart, FB, p.K, gst, tstart, ent);
+  SV_HIP(hipMemcpyAsync(gst + p.nbt, bstart + nwb, 4, hipMemcpyDeviceToDevice, st));
   SV_HIP(hipGetLastError());
   SV_HIP(hipEventRecord(ev[2], st));
   hipLaunchKernelGGL(k_accumulate, dim3(cdiv(p.T, kBlock)), dim3(kBlock), 0, st, bases, ent, gst,
@@ -587,10 +709,9 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
   hipLaunchKernelGGL(k_wsum, dim3(cdiv((uint64_t)p.J * p.W, kBlock)), dim3(kBlock), 0, st, bsum, p.B, p.J,
                      p.W, 1, racc, rtot);
   hipLaunchKernelGGL(k_group_sum, dim3(p.NG * p.W), dim3(kGroupBlock), 0, st, racc, rtot, p.J, p.logJ, ping);
-  const G1Xyzz* src = ping;
   SV_HIP(hipGetLastError());
   SV_HIP(hipEventRecord(ev[5], st));
-  SV_HIP(hipMemcpyAsync(ws->pinned, src, nfinal * sizeof(G1Xyzz), hipMemcpyDeviceToHost, st));
+  SV_HIP(hipMemcpyAsync(ws->pinned, ping, nfinal * sizeof(G1Xyzz), hipMemcpyDeviceToHost, st));
   SV_HIP(hipMemcpyAsync(ws->pinned + nfinal * sizeof(G1Xyzz), err, 4, hipMemcpyDeviceToHost, st));
   SV_HIP(hipStreamSynchronize(st));
   uint32_t errv;
@@ -607,7 +728,7 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
   sv_msm_stats& s = g_last_stats;
   float ms;
   hipEventElapsedTime(&ms, ev[0], ev[1]);
-  s.digits_ms = ms;
+  s.digits_ms = ms;  // digits + coarse histogram (digits are recomputed, never stored)
   hipEventElapsedTime(&ms, ev[1], ev[2]);
   s.sort_ms = ms;
   hipEventElapsedTime(&ms, ev[2], ev[3]);

@@ -29,6 +29,7 @@ struct Workspace {
   static constexpr int kEvents = 24;
   hipEvent_t ev[kEvents] = {};
 
+
   // carve `bytes` from the device buffer (256-B aligned); call reserve() first
   template <class T>
   T* carve(size_t count) {

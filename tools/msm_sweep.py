@@ -16,7 +16,9 @@ for log_n in log_ns:
     ref = None
     for c in [int(x) for x in os.environ.get("SWEEP_C", "14,15,16").split(",")]:
         for K in [int(x) for x in os.environ.get("SWEEP_K", "32,64,128").split(",")]:
-            os.environ["SVGPU_WINDOW_BITS"] = str(c); os.environ["SVGPU_ACC_K"] = str(K)
+            os.environ["SVGPU_WINDOW_BITS"] = str(c)
+            if K: os.environ["SVGPU_ACC_K"] = str(K)
+            else: os.environ.pop("SVGPU_ACC_K", None)
             r = dv.msm(B, S)
             if ref is None: ref = r
             ts = []

@@ -57,6 +57,7 @@ struct Grp {
   int s;          // sub-lane
   bool w;         // writer (s == 0, active)
   SqrTerm sq[4];  // this lane's square terms (slots s, s + S, ...), kept in registers
+  SqrTerm sqh;    // S = 8 half-product squaring: term s >> 1 of coefficient k
 };
 
 template <int S>
@@ -141,6 +142,64 @@ __device__ __forceinline__ Fq2 g_line(const Grp& G, const Fq2& x, const Fq2& l0,
   return sub_reduce<S>(lo + fq2_mul_xi(hi));
 }
 
+// ---- S = 8 half-product forms: sub-lane s = 2t + h computes component h (0: re, 1: im) of term t
+// with two independent Fq products (re(xy) = x0 y0 - x1 y1, im(xy) = x0 y1 + x1 y0) instead of a
+// whole Karatsuba Fq2 product (3 dependent-issue products), and its contribution to the
+// coefficient: plain (v, 0) / (0, v); wrapped terms carry xi: xi (a + b u) = (9a - b) + (a + 9b) u,
+// so a re-lane adds (9v, v) and an im-lane (-v, 9v).  Control flow stays uniform: idle lanes
+// compute on slot 0 and contribute zero.
+__device__ __forceinline__ Fq fq_mul9(const Fq& a) {
+  const Fq a2 = a + a, a4 = a2 + a2;
+  return a4 + a4 + a;
+}
+
+__device__ __forceinline__ Fq2 half_term(const Fq2& x, const Fq2& y, int h, bool xi, bool live) {
+  const Fq m1 = x.c0 * (h ? y.c1 : y.c0);
+  const Fq m2 = x.c1 * (h ? y.c0 : y.c1);
+  const Fq v = h ? m1 + m2 : m1 - m2;
+  const Fq v9 = fq_mul9(v);
+  Fq cr, ci;
+  if (!xi) {
+    cr = h ? Fq::zero() : v;
+    ci = h ? v : Fq::zero();
+  } else {
+    cr = h ? -v : v9;
+    ci = h ? v9 : v;
+  }
+  if (!live) cr = ci = Fq::zero();
+  return {cr, ci};
+}
+
+template <int S>
+__device__ __forceinline__ Fq2 g_sqr_h(const Grp& G, const Fq2& x) {
+  static_assert(S == 8, "half-product squaring needs 8 sub-lanes");
+  if (G.w) G.a[G.k] = x;
+  __syncthreads();
+  const SqrTerm q = G.sqh;
+  const bool live = q.i >= 0;
+  const Fq2 X = G.a[live ? q.i : 0], Y = G.a[live ? q.j : 0];
+  Fq2 c = half_term(X, Y, G.s & 1, q.xi, live);
+  if (q.dbl) c = c + c;
+  __syncthreads();
+  return sub_reduce<S>(c);
+}
+
+// f * (l0 + l1 w + l3 w^3): terms t = 0, 1, 2 take f_k, f_{k-1}, f_{k-3} (wrapping with xi)
+template <int S>
+__device__ __forceinline__ Fq2 g_line_h(const Grp& G, const Fq2& x, const Fq2& l0, const Fq2& l1, const Fq2& l3) {
+  static_assert(S == 8, "half-product line step needs 8 sub-lanes");
+  if (G.w) G.a[G.k] = x;
+  __syncthreads();
+  const int t = G.s >> 1;
+  const bool live = t < 3;
+  const int sh = t == 0 ? 0 : (t == 1 ? 1 : 3);
+  const int src = G.k - sh;
+  const Fq2& l = t == 0 ? l0 : (t == 1 ? l1 : l3);
+  const Fq2 c = half_term(G.a[live ? (src < 0 ? src + 6 : src) : 0], l, G.s & 1, src < 0, live);
+  __syncthreads();
+  return sub_reduce<S>(c);
+}
+
 __device__ __forceinline__ Fq2 g_conj(const Grp& G, const Fq2& x) { return (G.k & 1) ? -x : x; }
 __device__ __forceinline__ Fq2 g_frob(const Grp& G, int n, const Fq2& x) {
   Fq2 y = (n & 1) ? fq2_conj(x) : x;
@@ -164,21 +223,36 @@ __device__ __noinline__ Fq2 g_inv(const Grp& G, const Fq2& x) {
   Fq12 fi = fq12_inv(f);
   return tower_coeff(fi, G.k);
 }
+// Squaring / line steps: the half-product forms at S = 8, the whole-product forms otherwise
+// (measured per op on one wave, tools/ubench_decops.hip: g_sqr 4.8 us, g_sqr_h 3.2 us; a Granger-Scott
+// cyclotomic squaring with one product level measured 6.1 us -- single-wave code is bound by
+// dependent-instruction latency, and its many Fq2 additions cost more than the products it saves)
 template <int S>
-__device__ __noinline__ Fq2 g_pow_x(const Grp& G, const Fq2& a) {
+__device__ __forceinline__ Fq2 g_msq(const Grp& G, const Fq2& x) {
+  if constexpr (S == 8) return g_sqr_h<S>(G, x);
+  else return g_sqr<S>(G, x);
+}
+template <int S>
+__device__ __forceinline__ Fq2 g_mline(const Grp& G, const Fq2& x, const Fq2& l0, const Fq2& l1, const Fq2& l3) {
+  if constexpr (S == 8) return g_line_h<S>(G, x, l0, l1, l3);
+  else return g_line<S>(G, x, l0, l1, l3);
+}
+
+template <int S>
+__device__ __forceinline__ Fq2 g_pow_x(const Grp& G, const Fq2& a) {
   Fq2 r = a;
   for (int b = 61; b >= 0; b--) {
-    r = g_sqr<S>(G, r);
+    r = g_msq<S>(G, r);
     if ((BN_X >> b) & 1) r = g_mul<S>(G, r, a);
   }
   return r;
 }
 template <int S>
-__device__ __noinline__ Fq2 g_pow_small(const Grp& G, const Fq2& a, uint32_t e) {
+__device__ __forceinline__ Fq2 g_pow_small(const Grp& G, const Fq2& a, uint32_t e) {
   Fq2 r = a;
   const int top = 31 - __builtin_clz(e);
   for (int b = top - 1; b >= 0; b--) {
-    r = g_sqr<S>(G, r);
+    r = g_msq<S>(G, r);
     if ((e >> b) & 1) r = g_mul<S>(G, r, a);
   }
   return r;
@@ -223,7 +297,8 @@ __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ l
   const bool active = gl < 6 * S;
   const int k = active ? gl / S : 5, sub = active ? gl % S : 0;
   const uint32_t acc = blockIdx.x * NGRP + grp;
-  Grp G{sh + grp * 12, sh + grp * 12 + 6, k, sub, active && sub == 0, {}};
+  Grp G{sh + grp * 12, sh + grp * 12 + 6, k, sub, active && sub == 0, {}, {}};
+  G.sqh = (S == 8 && active) ? c_sqr[k][sub >> 1] : SqrTerm{-1, -1, 0, 0};
 #pragma unroll
   for (int t = 0; t < 4; t++) {
     const int slot = t * S + sub;
@@ -241,19 +316,19 @@ __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ l
   Fq2 f = G.k == 0 ? Fq2::one() : Fq2::zero();
   int idx = 0;
   for (int i = ATE_NAF_LEN - 1; i >= 1 && (phases & 1); i--) {
-    if (i != ATE_NAF_LEN - 1) f = g_sqr<S>(G, f);
-    f = g_line<S>(G, f, E[2 * idx].c0, E[2 * idx].c3, E[2 * idx].c4);
-    f = g_line<S>(G, f, E[2 * idx + 1].c0, E[2 * idx + 1].c3, E[2 * idx + 1].c4);
+    if (i != ATE_NAF_LEN - 1) f = g_msq<S>(G, f);
+    f = g_mline<S>(G, f, E[2 * idx].c0, E[2 * idx].c3, E[2 * idx].c4);
+    f = g_mline<S>(G, f, E[2 * idx + 1].c0, E[2 * idx + 1].c3, E[2 * idx + 1].c4);
     idx++;
     if (c_naf[i - 1] != 0) {
-      f = g_line<S>(G, f, E[2 * idx].c0, E[2 * idx].c3, E[2 * idx].c4);
-      f = g_line<S>(G, f, E[2 * idx + 1].c0, E[2 * idx + 1].c3, E[2 * idx + 1].c4);
+      f = g_mline<S>(G, f, E[2 * idx].c0, E[2 * idx].c3, E[2 * idx].c4);
+      f = g_mline<S>(G, f, E[2 * idx + 1].c0, E[2 * idx + 1].c3, E[2 * idx + 1].c4);
       idx++;
     }
   }
   for (int st = 0; st < 2 && (phases & 1); st++) {
-    f = g_line<S>(G, f, E[2 * idx].c0, E[2 * idx].c3, E[2 * idx].c4);
-    f = g_line<S>(G, f, E[2 * idx + 1].c0, E[2 * idx + 1].c3, E[2 * idx + 1].c4);
+    f = g_mline<S>(G, f, E[2 * idx].c0, E[2 * idx].c3, E[2 * idx].c4);
+    f = g_mline<S>(G, f, E[2 * idx + 1].c0, E[2 * idx + 1].c3, E[2 * idx + 1].c4);
     idx++;
   }
   // final exponentiation (same chain as curve.hpp final_exponentiation)
@@ -271,7 +346,7 @@ __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ l
   Fq2 t = g_mul<S>(G, g_mul<S>(G, fx3_36, g_pow_small<S>(G, fx2, 18)), g_pow_small<S>(G, fx, 12));
   Fq2 l1v = g_mul<S>(G, g_conj(G, t), f);
   t = g_mul<S>(G, g_mul<S>(G, g_mul<S>(G, fx3_36, g_pow_small<S>(G, fx2, 30)), g_pow_small<S>(G, fx, 18)),
-               g_sqr<S>(G, f));
+               g_msq<S>(G, f));
   Fq2 l0v = g_conj(G, t);
   e = g_mul<S>(G, g_mul<S>(G, g_mul<S>(G, l0v, g_frob(G, 1, l1v)), g_frob(G, 2, l2v)), g_frob(G, 3, f));
   }

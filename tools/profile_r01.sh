@@ -11,8 +11,8 @@ step() {  # name timeout cmd...
   echo "[$name] rc=$rc"; tail -3 "gpurun_out/prof/$name.log"
   if [ $rc -ne 0 ]; then echo "stopping"; exit $rc; fi
 }
-step trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extras
+step trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extras --config4-log-n 0
 step trace_extras 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace_extras -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
-step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras
-step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof/pmc_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras
+step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --config4-log-n 0
+step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof/pmc_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --config4-log-n 0
 find gpurun_out/prof -name "*.csv" | head -20

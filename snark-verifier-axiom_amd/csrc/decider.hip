@@ -53,6 +53,8 @@ __constant__ int8_t c_naf[ATE_NAF_LEN] = SV_ATE_NAF_INIT;
 struct Grp {
   Fq2* a;         // this group's 6 LDS slots for operand A
   Fq2* b;         // ... and operand B
+  Fq2* tab;       // kTab x 6 LDS slots: odd powers (and conjugates) for the windowed x-power
+  Fq2* keep;      // kKeep x 6 LDS slots: long-lived final-exponentiation values
   int k;          // coefficient index (lanes past 6*S mirror k = 5 and never write)
   int s;          // sub-lane
   bool w;         // writer (s == 0, active)
@@ -60,19 +62,34 @@ struct Grp {
   SqrTerm sqh;    // S = 8 half-product squaring: term s >> 1 of coefficient k
 };
 
+// Cross-lane moves inside 8-lane sub-lane groups by DPP (a VALU operand modifier, no LDS round
+// trip like the ds_bpermute behind __shfl_xor): level 1 swaps lane pairs (quad_perm [1,0,3,2]),
+// level 2 swaps pairs of pairs (quad_perm [2,3,0,1]); after those every lane of a quad holds the
+// quad's sum, so level 3 only needs the other quad of the 8: row_half_mirror (lane i <- 7 - i).
+template <int LEVEL>
+__device__ __forceinline__ uint32_t dpp_partner(uint32_t x) {
+  constexpr int ctrl = LEVEL == 0 ? 0xB1 : (LEVEL == 1 ? 0x4E : 0x141);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, ctrl, 0xF, 0xF, false);
+}
+
+template <int LEVEL>
+__device__ __forceinline__ Fq2 dpp_partner(const Fq2& v) {
+  Fq2 o;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    o.c0.v[i] = dpp_partner<LEVEL>(v.c0.v[i]);
+    o.c1.v[i] = dpp_partner<LEVEL>(v.c1.v[i]);
+  }
+  return o;
+}
+
 template <int S>
 __device__ __forceinline__ Fq2 sub_reduce(Fq2 v) {
-  // sum over the S consecutive sub-lanes of one coefficient (S = 1, 2, 4)
-#pragma unroll
-  for (int m = 1; m < S; m <<= 1) {
-    Fq2 o;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      o.c0.v[i] = __shfl_xor(v.c0.v[i], m);
-      o.c1.v[i] = __shfl_xor(v.c1.v[i], m);
-    }
-    v = v + o;
-  }
+  // sum over the S consecutive sub-lanes of one coefficient (S = 1, 2, 4, 8; groups 8-aligned)
+  static_assert(S == 1 || S == 2 || S == 4 || S == 8, "sub-lane count");
+  if constexpr (S >= 2) v = v + dpp_partner<0>(v);
+  if constexpr (S >= 4) v = v + dpp_partner<1>(v);
+  if constexpr (S >= 8) v = v + dpp_partner<2>(v);
   return v;
 }
 
@@ -238,22 +255,79 @@ __device__ __forceinline__ Fq2 g_mline(const Grp& G, const Fq2& x, const Fq2& l0
   else return g_line<S>(G, x, l0, l1, l3);
 }
 
+// f * y with y's six coefficients already in LDS (yb[0..5]): no operand write on the critical path
 template <int S>
-__device__ __forceinline__ Fq2 g_pow_x(const Grp& G, const Fq2& a) {
-  Fq2 r = a;
-  for (int b = 61; b >= 0; b--) {
-    r = g_msq<S>(G, r);
-    if ((BN_X >> b) & 1) r = g_mul<S>(G, r, a);
+__device__ __forceinline__ Fq2 g_mul_lds(const Grp& G, const Fq2& x, const Fq2* yb) {
+  if (G.w) G.a[G.k] = x;
+  __syncthreads();
+  Fq2 lo = Fq2::zero(), hi = Fq2::zero();
+#pragma unroll
+  for (int t = 0; t < (6 + S - 1) / S; t++) {
+    const int i = t * S + G.s;
+    if (i < 6) {
+      const int j = G.k - i;
+      const Fq2 p = G.a[i] * yb[j < 0 ? j + 6 : j];
+      if (j >= 0) lo = lo + p;
+      else hi = hi + p;
+    }
   }
+  __syncthreads();
+  return sub_reduce<S>(lo + fq2_mul_xi(hi));
+}
+
+__device__ __forceinline__ void g_put(const Grp& G, Fq2* slots, int e, const Fq2& v) {
+  if (G.w) slots[e * 6 + G.k] = v;
+}
+__device__ __forceinline__ Fq2 g_get(const Grp& G, const Fq2* slots, int e) { return slots[e * 6 + G.k]; }
+
+// x = 0x44e992b44a6909f1 in width-4 NAF (odd digits in [-7, 7], 14 non-zero of 63): 62 squarings
+// and 13 multiplications by a tabulated odd power instead of 27 for plain binary.  Negative digits
+// multiply by the conjugate, which is the inverse on the cyclotomic subgroup the hard part of the
+// final exponentiation works in.
+struct XNaf {
+  int8_t d[66];
+  int len;
+};
+constexpr XNaf make_xnaf() {
+  XNaf r{};
+  uint64_t k = BN_X;
+  int i = 0;
+  while (k) {
+    int v = 0;
+    if (k & 1) {
+      v = (int)(k & 15);
+      if (v >= 8) v -= 16;
+      k = v >= 0 ? k - (uint64_t)v : k + (uint64_t)(-v);
+    }
+    r.d[i++] = (int8_t)v;
+    k >>= 1;
+  }
+  r.len = i;
   return r;
 }
+__constant__ XNaf c_xnaf = make_xnaf();
+static constexpr int kTab = 8;   // a, a^3, a^5, a^7, then their conjugates
+static constexpr int kKeep = 6;
+
 template <int S>
-__device__ __forceinline__ Fq2 g_pow_small(const Grp& G, const Fq2& a, uint32_t e) {
-  Fq2 r = a;
-  const int top = 31 - __builtin_clz(e);
-  for (int b = top - 1; b >= 0; b--) {
+__device__ __forceinline__ Fq2 g_pow_x(const Grp& G, const Fq2& a) {
+  const Fq2 a2 = g_msq<S>(G, a);
+  g_put(G, G.tab, 0, a);
+  g_put(G, G.tab, 4, g_conj(G, a));
+  Fq2 ak = a;
+  for (int e = 1; e < 4; e++) {
+    ak = g_mul<S>(G, ak, a2);
+    g_put(G, G.tab, e, ak);
+    g_put(G, G.tab, 4 + e, g_conj(G, ak));
+  }
+  __syncthreads();  // the last table entries are read below without an intervening exchange
+  const int len = c_xnaf.len;
+  const int top = c_xnaf.d[len - 1];
+  Fq2 r = g_get(G, G.tab, top > 0 ? (top - 1) / 2 : 4 + (-top - 1) / 2);
+  for (int i = len - 2; i >= 0; i--) {
     r = g_msq<S>(G, r);
-    if ((e >> b) & 1) r = g_mul<S>(G, r, a);
+    const int d = c_xnaf.d[i];
+    if (d) r = g_mul_lds<S>(G, r, G.tab + 6 * (d > 0 ? (d - 1) / 2 : 4 + (-d - 1) / 2));
   }
   return r;
 }
@@ -293,11 +367,12 @@ __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ l
   constexpr int NGRP = 64 / GL;     // groups per single-wave block
   __shared__ Fq2 sh[2 * NGRP * 6];
   __shared__ LineCoeff ev[NGRP][2 * ATE_NUM_LINES];
+  __shared__ Fq2 tabk[NGRP][(kTab + kKeep) * 6];
   const int lane = threadIdx.x, grp = lane / GL, gl = lane % GL;
   const bool active = gl < 6 * S;
   const int k = active ? gl / S : 5, sub = active ? gl % S : 0;
   const uint32_t acc = blockIdx.x * NGRP + grp;
-  Grp G{sh + grp * 12, sh + grp * 12 + 6, k, sub, active && sub == 0, {}, {}};
+  Grp G{sh + grp * 12, sh + grp * 12 + 6, tabk[grp], tabk[grp] + kTab * 6, k, sub, active && sub == 0, {}, {}};
   G.sqh = (S == 8 && active) ? c_sqr[k][sub >> 1] : SqrTerm{-1, -1, 0, 0};
 #pragma unroll
   for (int t = 0; t < 4; t++) {
@@ -338,16 +413,36 @@ __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ l
   Fq2 fi = g_inv(G, f);
   f = g_mul<S>(G, g_conj(G, f), fi);
   f = g_mul<S>(G, g_frob(G, 2, f), f);
-  Fq2 fx = g_pow_x<S>(G, f);
-  Fq2 fx2 = g_pow_x<S>(G, fx);
-  Fq2 fx3 = g_pow_x<S>(G, fx2);
-  Fq2 fx3_36 = g_pow_small<S>(G, fx3, 36);
-  Fq2 l2v = g_mul<S>(G, g_pow_small<S>(G, fx2, 6), f);
-  Fq2 t = g_mul<S>(G, g_mul<S>(G, fx3_36, g_pow_small<S>(G, fx2, 18)), g_pow_small<S>(G, fx, 12));
-  Fq2 l1v = g_mul<S>(G, g_conj(G, t), f);
-  t = g_mul<S>(G, g_mul<S>(G, g_mul<S>(G, fx3_36, g_pow_small<S>(G, fx2, 30)), g_pow_small<S>(G, fx, 18)),
-               g_msq<S>(G, f));
-  Fq2 l0v = g_conj(G, t);
+  // hard part: f^(l0 + l1 p + l2 p^2 + p^3) with the x-power chain; the small powers of fx and
+  // fx^2 share their ladders (fx^6 -> fx^12 -> fx^18, fx2^6 -> fx2^12 -> fx2^18 -> fx2^30)
+  enum { K_F, K_B12, K_B18, K_A6, K_A18, K_A30 };
+  g_put(G, G.keep, K_F, f);
+  const Fq2 fx = g_pow_x<S>(G, f);
+  {
+    const Fq2 b6 = g_msq<S>(G, g_mul<S>(G, g_msq<S>(G, fx), fx));
+    const Fq2 b12 = g_msq<S>(G, b6);
+    g_put(G, G.keep, K_B12, b12);
+    g_put(G, G.keep, K_B18, g_mul<S>(G, b12, b6));
+  }
+  const Fq2 fx2 = g_pow_x<S>(G, fx);
+  {
+    const Fq2 a6 = g_msq<S>(G, g_mul<S>(G, g_msq<S>(G, fx2), fx2));
+    const Fq2 a12 = g_msq<S>(G, a6);
+    const Fq2 a18 = g_mul<S>(G, a12, a6);
+    g_put(G, G.keep, K_A6, a6);
+    g_put(G, G.keep, K_A18, a18);
+    g_put(G, G.keep, K_A30, g_mul<S>(G, a18, a12));
+  }
+  const Fq2 fx3 = g_pow_x<S>(G, fx2);
+  Fq2 y = g_msq<S>(G, g_msq<S>(G, g_msq<S>(G, fx3)));        // fx3^8
+  const Fq2 y36 = g_msq<S>(G, g_msq<S>(G, g_mul<S>(G, y, fx3)));  // fx3^36
+  f = g_get(G, G.keep, K_F);
+  const Fq2 l2v = g_mul_lds<S>(G, f, G.keep + 6 * K_A6);
+  Fq2 t = g_mul_lds<S>(G, g_mul_lds<S>(G, y36, G.keep + 6 * K_A18), G.keep + 6 * K_B12);
+  const Fq2 l1v = g_mul_lds<S>(G, g_conj(G, t), G.keep + 6 * K_F);
+  t = g_mul_lds<S>(G, g_mul_lds<S>(G, y36, G.keep + 6 * K_A30), G.keep + 6 * K_B18);
+  t = g_mul<S>(G, t, g_msq<S>(G, f));
+  const Fq2 l0v = g_conj(G, t);
   e = g_mul<S>(G, g_mul<S>(G, g_mul<S>(G, l0v, g_frob(G, 1, l1v)), g_frob(G, 2, l2v)), g_frob(G, 3, f));
   }
   const bool one_k = G.k == 0 ? (e == Fq2::one()) : e.is_zero();

@@ -14,7 +14,7 @@ __global__ void __launch_bounds__(64) k_op(int iters, Fq2* out) {
   const int lane = threadIdx.x;
   const bool active = lane < 6 * S;
   const int k = active ? lane / S : 5, sub = active ? lane % S : 0;
-  Grp G{sh, sh + 6, k, sub, active && sub == 0, {}, {}};
+  Grp G{sh, sh + 6, nullptr, nullptr, k, sub, active && sub == 0, {}, {}};
 #pragma unroll
   for (int t = 0; t < 4; t++) {
     const int slot = t * S + sub;

@@ -173,7 +173,7 @@ __device__ __forceinline__ Fq fq_mul9(const Fq& a) {
 __device__ __forceinline__ Fq2 half_term(const Fq2& x, const Fq2& y, int h, bool xi, bool live) {
   const Fq m1 = x.c0 * (h ? y.c1 : y.c0);
   const Fq m2 = x.c1 * (h ? y.c0 : y.c1);
-  const Fq v = h ? m1 + m2 : m1 - m2;
+  const Fq v = h ? m1 + m2 : fe_sub_lat(m1, m2);
   const Fq v9 = fq_mul9(v);
   Fq cr, ci;
   if (!xi) {

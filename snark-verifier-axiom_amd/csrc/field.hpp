@@ -95,17 +95,22 @@ SV_HD Fe<M> fe_select(bool c, const Fe<M>& a, const Fe<M>& b) {
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
-// Device add/sub as explicit carry chains (__builtin_addc/subc -> v_addc/v_subb through VCC, hazard
-// padding by the compiler): 32 VALU per op instead of ~90 for the 64-bit-intermediate C form.
+// Device add/sub as explicit carry chains (__builtin_addc/subc -> v_addc/v_subb through an SGPR pair,
+// 32 VALU per op instead of ~90 for the 64-bit-intermediate C form).  A VALU carry-out read by the
+// next v_addc needs two wait states, so a lone chain issues one useful instruction per three slots;
+// the loops below are fused so the compiler interleaves independent chains (the trial subtraction
+// of p lags the addition by one limb) and the wait states fill with useful work -- this matters
+// for the single-wave latency-bound code (decider, Horner chains, tails).
 template <class M>
 SV_HD Fe<M> operator+(const Fe<M>& a, const Fe<M>& b) {
   Fe<M> t, d, r;
   uint32_t c = 0, br = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) t.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
-  // a + b < 2p < 2^255: no carry out; subtract p when t >= p
-#pragma unroll
-  for (int i = 0; i < 8; i++) d.v[i] = __builtin_subc(t.v[i], M::p(i), br, &br);
+  for (int i = 0; i < 8; i++) {
+    t.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+    // a + b < 2p < 2^255: no carry out; subtract p when t >= p
+    d.v[i] = __builtin_subc(t.v[i], M::p(i), br, &br);
+  }
 #pragma unroll
   for (int i = 0; i < 8; i++) r.v[i] = br ? t.v[i] : d.v[i];
   return r;
@@ -120,6 +125,23 @@ SV_HD Fe<M> operator-(const Fe<M>& a, const Fe<M>& b) {
   const uint32_t mask = 0u - br;  // add p back on borrow
 #pragma unroll
   for (int i = 0; i < 8; i++) r.v[i] = __builtin_addc(t.v[i], M::p(i) & mask, c, &c);
+  return r;
+}
+
+// Latency form of a - b for chains that run on a single wave: a - b and a + (p - b) as three
+// independent carry chains (no wait for the final borrow before the correction), then a select.
+template <class M>
+SV_HD Fe<M> fe_sub_lat(const Fe<M>& a, const Fe<M>& b) {
+  Fe<M> t, w, u, r;
+  uint32_t b1 = 0, b2 = 0, c3 = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    t.v[i] = __builtin_subc(a.v[i], b.v[i], b1, &b1);
+    w.v[i] = __builtin_subc(M::p(i), b.v[i], b2, &b2);
+    u.v[i] = __builtin_addc(a.v[i], w.v[i], c3, &c3);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = b1 ? u.v[i] : t.v[i];
   return r;
 }
 #else
@@ -170,11 +192,29 @@ SV_HD Fe<M> operator-(const Fe<M>& a, const Fe<M>& b) {
   return r;
 }
 
+template <class M>
+SV_HD Fe<M> fe_sub_lat(const Fe<M>& a, const Fe<M>& b) {
+  return a - b;
+}
 #endif
 
 template <class M>
 SV_HD Fe<M> operator-(const Fe<M>& a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // p - a with one borrow chain; -0 = 0
+  Fe<M> r;
+  uint32_t br = 0, nz = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    r.v[i] = __builtin_subc(M::p(i), a.v[i], br, &br);
+    nz |= a.v[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = nz ? r.v[i] : 0u;
+  return r;
+#else
   return Fe<M>::zero() - a;
+#endif
 }
 
 template <class M>
@@ -470,8 +510,50 @@ struct Fq2 {
   SV_HD bool operator==(const Fq2& o) const { return c0 == o.c0 && c1 == o.c1; }
 };
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// both components' chains in one loop (four independent carry chains interleave, see Fe add)
+SV_HD Fq2 operator+(const Fq2& a, const Fq2& b) {
+  Fq t0, t1, d0, d1;
+  uint32_t c0 = 0, c1 = 0, e0 = 0, e1 = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    t0.v[i] = __builtin_addc(a.c0.v[i], b.c0.v[i], c0, &c0);
+    t1.v[i] = __builtin_addc(a.c1.v[i], b.c1.v[i], c1, &c1);
+    d0.v[i] = __builtin_subc(t0.v[i], FQ_P[i], e0, &e0);
+    d1.v[i] = __builtin_subc(t1.v[i], FQ_P[i], e1, &e1);
+  }
+  Fq2 r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    r.c0.v[i] = e0 ? t0.v[i] : d0.v[i];
+    r.c1.v[i] = e1 ? t1.v[i] : d1.v[i];
+  }
+  return r;
+}
+SV_HD Fq2 operator-(const Fq2& a, const Fq2& b) {
+  Fq t0, t1, w0, w1, u0, u1;
+  uint32_t b0 = 0, b1 = 0, x0 = 0, x1 = 0, c0 = 0, c1 = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    t0.v[i] = __builtin_subc(a.c0.v[i], b.c0.v[i], b0, &b0);
+    t1.v[i] = __builtin_subc(a.c1.v[i], b.c1.v[i], b1, &b1);
+    w0.v[i] = __builtin_subc(FQ_P[i], b.c0.v[i], x0, &x0);
+    w1.v[i] = __builtin_subc(FQ_P[i], b.c1.v[i], x1, &x1);
+    u0.v[i] = __builtin_addc(a.c0.v[i], w0.v[i], c0, &c0);
+    u1.v[i] = __builtin_addc(a.c1.v[i], w1.v[i], c1, &c1);
+  }
+  Fq2 r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    r.c0.v[i] = b0 ? u0.v[i] : t0.v[i];
+    r.c1.v[i] = b1 ? u1.v[i] : t1.v[i];
+  }
+  return r;
+}
+#else
 SV_HD Fq2 operator+(const Fq2& a, const Fq2& b) { return {a.c0 + b.c0, a.c1 + b.c1}; }
 SV_HD Fq2 operator-(const Fq2& a, const Fq2& b) { return {a.c0 - b.c0, a.c1 - b.c1}; }
+#endif
 SV_HD Fq2 operator-(const Fq2& a) { return {-a.c0, -a.c1}; }
 SV_HD Fq2 operator*(const Fq2& a, const Fq2& b) {
   Fq t0 = a.c0 * b.c0;

@@ -35,6 +35,9 @@ __global__ void __launch_bounds__(64) k_op(int iters, Fq2* out) {
     if constexpr (OP == 7) f = f * l;         // one lane-local Fq2 product (Karatsuba)
     if constexpr (OP == 8) f.c0 = f.c0 * l.c1;  // one Fq product
     if constexpr (OP == 9) f = sub_reduce<S>(f);
+    if constexpr (OP == 10) f.c0 = fe_inv(f.c0);
+    if constexpr (OP == 11) f.c0 = fq_mul9(f.c0);
+    if constexpr (OP == 12) f = f + l;
   }
   if (G.w) out[blockIdx.x * 6 + k] = f;
 }
@@ -58,9 +61,9 @@ int main() {
   Fq2* d;
   hipMalloc(&d, 4096 * 6 * sizeof(Fq2));
   const char* names[] = {"g_sqr", "g_sqr_h", "(unused)", "g_mul", "g_line", "g_line_h", "g_inv",
-                         "Fq2 mul (lane)", "Fq mul (lane)", "sub_reduce<8>"};
-  for (int blocks : {1, 256}) {
-    float t[10];
+                         "Fq2 mul (lane)", "Fq mul (lane)", "sub_reduce<8>", "fe_inv", "fq_mul9", "Fq2 add"};
+  for (int blocks : {1}) {
+    float t[13];
     t[0] = run<0>(blocks, 200, d);
     t[1] = run<1>(blocks, 200, d);
     t[2] = 0.f;
@@ -71,7 +74,10 @@ int main() {
     t[7] = run<7>(blocks, 200, d);
     t[8] = run<8>(blocks, 200, d);
     t[9] = run<9>(blocks, 200, d);
-    for (int i = 0; i < 10; i++) printf("blocks=%d %-16s %8.3f us/op\n", blocks, names[i], t[i]);
+    t[10] = run<10>(blocks, 10, d);
+    t[11] = run<11>(blocks, 200, d);
+    t[12] = run<12>(blocks, 200, d);
+    for (int i = 0; i < 13; i++) printf("blocks=%d %-16s %8.3f us/op\n", blocks, names[i], t[i]);
   }
   return 0;
 }

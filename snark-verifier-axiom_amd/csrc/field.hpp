@@ -377,12 +377,7 @@ SV_HD Fe<M> fe_from_mont(const Fe<M>& a) {
   return a * o;
 }
 
-// Inverse in Montgomery form (0 -> 0) by the binary extended Euclidean algorithm (Guide to ECC,
-// alg. 2.22) on the raw integer aR: ~2 x 254 shift / subtract steps of plain integer VALU work,
-// about 5x shorter than the 254-squaring Fermat chain on one lane -- and inversions sit on serial
-// tails (affine conversion after a Horner chain, the decider's final exponentiation).  Inputs
-// are public (verifier data), so the data-dependent running time is harmless.
-// inv_raw(aR) = (aR)^-1; times R^3 (Montgomery) gives a^-1 R.
+// Multi-word helpers of the binary EEA inversion fe_inv_eea (kept as the host cross-check of fe_inv).
 namespace detail {
 SV_HD bool lw_is_one(const uint32_t* x) {
   uint32_t acc = x[0] ^ 1u;
@@ -451,8 +446,222 @@ SV_HD void lw_sub_mod(uint32_t* a, const uint32_t* b) {
 }
 }  // namespace detail
 
+// Inverse by batched divsteps (Bernstein-Yang "safegcd", variable-time form; restated from the
+// published algorithm): the low 32 bits of (f, g) drive up to 30 divsteps at a time, collected in a
+// 2x2 transition matrix that is then applied to the full-width (f, g) and to the Bezout
+// coefficients (d, e) mod m -- ~20 matrix applications of 9 signed 30-bit limbs instead of ~500
+// multi-word shift / subtract steps of the binary EEA.
+// Inputs are public verifier data, so the data-dependent running time is harmless.
+namespace detail {
+struct S30 {
+  int32_t v[9];
+};
+template <class M>
+struct ModInv30 {
+  S30 m;          // modulus in signed 30-bit limbs
+  uint32_t inv;   // modulus^-1 mod 2^30
+};
+constexpr uint32_t kM30 = 0x3fffffffu;
+template <class M>
+SV_HD S30 to_s30(const uint32_t* x) {
+  S30 r;
+  uint64_t acc = 0;
+  int bits = 0, k = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    acc |= (uint64_t)x[i] << bits;
+    bits += 32;
+    while (bits >= 30) {
+      r.v[k++] = (int32_t)(acc & kM30);
+      acc >>= 30;
+      bits -= 30;
+    }
+  }
+  r.v[8] = (int32_t)acc;  // 256 - 240 = 16 bits
+  return r;
+}
+SV_HD void from_s30(const S30& a, uint32_t* x) {  // a in [0, m), limbs normalised
+  uint64_t acc = 0;
+  int bits = 0, k = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    acc |= (uint64_t)(uint32_t)a.v[i] << bits;
+    bits += 30;
+    if (bits >= 32) {
+      x[k++] = (uint32_t)acc;
+      acc >>= 32;
+      bits -= 32;
+    }
+  }
+  if (k < 8) x[k] = (uint32_t)acc;
+}
+struct Trans {
+  int32_t u, v, q, r;
+};
+// up to 30 divsteps on the low words; returns the new eta (= -delta); t * [f, g] = 2^30 [f', g']
+SV_HD int32_t divsteps30(int32_t eta, uint32_t f0, uint32_t g0, Trans* t) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+  uint32_t f = f0, g = g0;
+  int i = 30;
+  for (;;) {
+    // divide g by 2 as often as possible (at most i more steps)
+    const uint32_t gs = g | (0xffffffffu << i);
+    const int zeros = __builtin_ctz(gs);
+    g >>= zeros;
+    u <<= zeros;
+    v <<= zeros;
+    eta -= zeros;
+    i -= zeros;
+    if (i == 0) break;
+    if (eta < 0) {  // delta > 0: (f, g) <- (g, -f)
+      eta = -eta;
+      uint32_t tmp = f;
+      f = g;
+      g = 0u - tmp;
+      tmp = u;
+      u = q;
+      q = 0u - tmp;
+      tmp = v;
+      v = r;
+      r = 0u - tmp;
+    }
+    // cancel the bottom min(eta + 1, i, 12) bits of g with a multiple of f (f odd)
+    int limit = eta + 1 > i ? i : eta + 1;
+    if (limit > 12) limit = 12;
+    const uint32_t m = 0xffffffffu >> (32 - limit);
+    uint32_t finv = f;                 // f^-1 mod 2^3
+    finv *= 2u - f * finv;             // mod 2^6
+    finv *= 2u - f * finv;             // mod 2^12
+    const uint32_t w = (0u - g * finv) & m;
+    g += f * w;
+    q += u * w;
+    r += v * w;
+  }
+  t->u = (int32_t)u;
+  t->v = (int32_t)v;
+  t->q = (int32_t)q;
+  t->r = (int32_t)r;
+  return eta;
+}
+// [f, g] <- t [f, g] / 2^30 over the first len limbs
+SV_HD void update_fg(int len, S30& f, S30& g, const Trans& t) {
+  int64_t cf = (int64_t)t.u * f.v[0] + (int64_t)t.v * g.v[0];
+  int64_t cg = (int64_t)t.q * f.v[0] + (int64_t)t.r * g.v[0];
+  cf >>= 30;
+  cg >>= 30;
+  for (int i = 1; i < len; i++) {
+    cf += (int64_t)t.u * f.v[i] + (int64_t)t.v * g.v[i];
+    cg += (int64_t)t.q * f.v[i] + (int64_t)t.r * g.v[i];
+    f.v[i - 1] = (int32_t)((uint32_t)cf & kM30);
+    g.v[i - 1] = (int32_t)((uint32_t)cg & kM30);
+    cf >>= 30;
+    cg >>= 30;
+  }
+  f.v[len - 1] = (int32_t)cf;
+  g.v[len - 1] = (int32_t)cg;
+}
+// [d, e] <- (t [d, e] + m [md, me]) / 2^30 with md, me chosen to clear the low 30 bits; d, e stay
+// in (-2m, m)
+SV_HD void update_de(S30& d, S30& e, const Trans& t, const S30& mod, uint32_t minv) {
+  const int32_t sd = d.v[8] >> 31, se = e.v[8] >> 31;
+  int32_t md = (t.u & sd) + (t.v & se);
+  int32_t me = (t.q & sd) + (t.r & se);
+  int64_t cd = (int64_t)t.u * d.v[0] + (int64_t)t.v * e.v[0];
+  int64_t ce = (int64_t)t.q * d.v[0] + (int64_t)t.r * e.v[0];
+  md -= (int32_t)((minv * (uint32_t)cd + (uint32_t)md) & kM30);
+  me -= (int32_t)((minv * (uint32_t)ce + (uint32_t)me) & kM30);
+  cd += (int64_t)mod.v[0] * md;
+  ce += (int64_t)mod.v[0] * me;
+  cd >>= 30;
+  ce >>= 30;
+#pragma unroll
+  for (int i = 1; i < 9; i++) {
+    cd += (int64_t)t.u * d.v[i] + (int64_t)t.v * e.v[i] + (int64_t)mod.v[i] * md;
+    ce += (int64_t)t.q * d.v[i] + (int64_t)t.r * e.v[i] + (int64_t)mod.v[i] * me;
+    d.v[i - 1] = (int32_t)((uint32_t)cd & kM30);
+    e.v[i - 1] = (int32_t)((uint32_t)ce & kM30);
+    cd >>= 30;
+    ce >>= 30;
+  }
+  d.v[8] = (int32_t)cd;
+  e.v[8] = (int32_t)ce;
+}
+// r in (-2m, m) -> (sign < 0 ? -r : r) mod m in [0, m), limbs normalised
+SV_HD void normalize30(S30& r, int32_t sign, const S30& mod) {
+  int32_t add = r.v[8] >> 31;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] += mod.v[i] & add;
+  const int32_t neg = sign >> 31;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = (r.v[i] ^ neg) - neg;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    r.v[i + 1] += r.v[i] >> 30;
+    r.v[i] &= (int32_t)kM30;
+  }
+  add = r.v[8] >> 31;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] += mod.v[i] & add;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    r.v[i + 1] += r.v[i] >> 30;
+    r.v[i] &= (int32_t)kM30;
+  }
+}
+// raw integer inverse x^-1 mod m (x in [1, m))
+template <class M>
+SV_HD void inv_raw(const uint32_t* x, uint32_t* out) {
+  uint32_t mw[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) mw[i] = M::p(i);
+  const S30 mod = to_s30<M>(mw);
+  uint32_t minv = mw[0];  // m^-1 mod 2^30 by Newton from m (odd)
+#pragma unroll
+  for (int k = 0; k < 5; k++) minv *= 2u - mw[0] * minv;
+  minv &= kM30;
+  S30 d{}, e{}, f = mod, g = to_s30<M>(x);
+  e.v[0] = 1;
+  int len = 9;
+  int32_t eta = -1;
+  for (;;) {
+    Trans t;
+    eta = divsteps30(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], &t);
+    update_de(d, e, t, mod, minv);
+    update_fg(len, f, g, t);
+    if (g.v[0] == 0) {
+      int32_t any = 0;
+      for (int j = 1; j < len; j++) any |= g.v[j];
+      if (any == 0) break;
+    }
+    const int32_t fn = f.v[len - 1], gn = g.v[len - 1];
+    int32_t cond = (len - 2) >> 31;
+    cond |= fn ^ (fn >> 31);
+    cond |= gn ^ (gn >> 31);
+    if (cond == 0) {  // top limbs are sign-only: shorten
+      f.v[len - 2] |= (int32_t)((uint32_t)fn << 30);
+      g.v[len - 2] |= (int32_t)((uint32_t)gn << 30);
+      len--;
+    }
+  }
+  normalize30(d, f.v[len - 1], mod);
+  from_s30(d, out);
+}
+}  // namespace detail
+
 template <class M>
 SV_NOINL Fe<M> fe_inv(const Fe<M>& a) {
+  if (a.is_zero()) return a;
+  Fe<M> r, r2;
+  detail::inv_raw<M>(a.v, r.v);  // (aR)^-1
+#pragma unroll
+  for (int i = 0; i < 8; i++) r2.v[i] = M::r2(i);
+  return r * (r2 * r2);  // (aR)^-1 * R^3 / R = a^-1 R
+}
+
+// Reference inversion (Guide to ECC alg. 2.22, binary EEA on the raw integer aR, ~2 x 254 shift /
+// subtract steps): tools/hostcheck_inv.cpp checks fe_inv against it.
+template <class M>
+SV_NOINL Fe<M> fe_inv_eea(const Fe<M>& a) {
   if (a.is_zero()) return a;
   uint32_t u[8], v[8], x1[8], x2[8];
 #pragma unroll

@@ -230,15 +230,32 @@ __device__ __forceinline__ Fq2 g_frob(const Grp& G, int n, const Fq2& x) {
   }
   return y * c;
 }
-__device__ __noinline__ Fq2 g_inv(const Grp& G, const Fq2& x) {
-  if (G.w) G.a[G.k] = x;
+// f^-1 = conj(f) N^-1 with N = f conj(f) = a^2 - v b^2 in Fq6 (f = a + b w over Fq6, v = w^2):
+// N sits on the even w-coefficients, its Fq6 inverse (t0 + t1 v + t2 v^2) / d is formed with the
+// three t_j on the lanes of coefficients 0, 2, 4 in parallel, and only the norm of d in Fq is
+// inverted (one fe_inv, on every lane, uniform) -- instead of a whole Fq12 inversion per lane.
+template <int S>
+__device__ __forceinline__ Fq2 g_inv(const Grp& G, const Fq2& f) {
+  const Fq2 fc = g_conj(G, f);
+  const Fq2 nk = g_mul<S>(G, f, fc);  // odd coefficients vanish
+  if (G.w) G.a[G.k] = nk;
   __syncthreads();
-  Fq12 f;
-#pragma unroll
-  for (int k = 0; k < 6; k++) tower_coeff(f, k) = G.a[k];
+  const Fq2 c0 = G.a[0], c1 = G.a[2], c2 = G.a[4];
+  const int j = G.k >> 1;
+  // t0 = c0^2 - xi c1 c2, t1 = xi c2^2 - c0 c1, t2 = c1^2 - c0 c2 (lanes of coefficient 2j)
+  const Fq2 x = j == 0 ? c0 : (j == 1 ? c2 : c1);
+  const Fq2 y0 = j == 0 ? c1 : c0, y1 = j == 0 ? c2 : (j == 1 ? c1 : c2);
+  const Fq2 sq = x * x, pr = y0 * y1;
+  const Fq2 tj = j == 0 ? sq - fq2_mul_xi(pr) : (j == 1 ? fq2_mul_xi(sq) - pr : sq - pr);
   __syncthreads();
-  Fq12 fi = fq12_inv(f);
-  return tower_coeff(fi, G.k);
+  if (G.w && !(G.k & 1)) G.b[j] = tj;
+  __syncthreads();
+  const Fq2 t0 = G.b[0], t1 = G.b[1], t2 = G.b[2];
+  __syncthreads();
+  const Fq2 d = c0 * t0 + fq2_mul_xi(c2 * t1 + c1 * t2);
+  const Fq2 di = fq2_inv(d);
+  const Fq2 ninv = (G.k & 1) ? Fq2::zero() : (j == 0 ? t0 : (j == 1 ? t1 : t2)) * di;
+  return g_mul<S>(G, fc, ninv);
 }
 // Squaring / line steps: the half-product forms at S = 8, the whole-product forms otherwise
 // (measured per op on one wave, tools/ubench_decops.hip: g_sqr 4.8 us, g_sqr_h 3.2 us; a Granger-Scott
@@ -410,7 +427,7 @@ __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ l
   // (phases: debug/profiling knob SVGPU_DECIDER_PHASES, 3 = both halves; results are only valid at 3)
   Fq2 e = f;
   if (phases & 2) {
-  Fq2 fi = g_inv(G, f);
+  Fq2 fi = g_inv<S>(G, f);
   f = g_mul<S>(G, g_conj(G, f), fi);
   f = g_mul<S>(G, g_frob(G, 2, f), f);
   // hard part: f^(l0 + l1 p + l2 p^2 + p^3) with the x-power chain; the small powers of fx and

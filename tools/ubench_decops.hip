@@ -31,7 +31,7 @@ __global__ void __launch_bounds__(64) k_op(int iters, Fq2* out) {
     if constexpr (OP == 3) f = g_mul<S>(G, f, l);
     if constexpr (OP == 4) f = g_line<S>(G, f, l, l, l);
     if constexpr (OP == 5) f = g_line_h<S>(G, f, l, l, l);
-    if constexpr (OP == 6) f = g_inv(G, f);
+    if constexpr (OP == 6) f = g_inv<S>(G, f);
     if constexpr (OP == 7) f = f * l;         // one lane-local Fq2 product (Karatsuba)
     if constexpr (OP == 8) f.c0 = f.c0 * l.c1;  // one Fq product
     if constexpr (OP == 9) f = sub_reduce<S>(f);

@@ -160,7 +160,7 @@ def test_adversarial_all_equal_scalars_2_18_is_fast(gpu, oracle_cpp):
     assert dt < 0.05, f"skewed-bucket MSM took {dt * 1e3:.1f} ms"
 
 
-@pytest.mark.parametrize("bits", [5, 9, 13, 14, 15])
+@pytest.mark.parametrize("bits", [4, 5, 9, 13, 14, 15, 16])
 def test_window_bits_override(gpu, oracle_cpp, bits, monkeypatch):
     """Every window size (incl. short top windows that concentrate digits) gives the same point."""
     import svgpu
@@ -169,3 +169,28 @@ def test_window_bits_override(gpu, oracle_cpp, bits, monkeypatch):
     B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=99)
     S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=99)
     assert svgpu.msm_arrays(B, S) == _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
+
+
+def test_edge_scalars(gpu, oracle_cpp):
+    """Scalars at window and GLV-decomposition edges (k = lambda gives k1 = 0, k2 = 1 in the
+    batched path's split; multiples and neighbours of lambda, of r, of 2^127 / 2^128) against the
+    reference Pippenger restatement."""
+    import random
+    import svgpu
+    from svgpu import encoding as enc
+    lam = 0xB3C4D79D41A917585BFC41088D8DAAA78B17EA66B99C90DD
+    r = b.R
+    ks = [0, 1, 2, lam, lam + 1, lam - 1, r - lam, (lam * lam) % r, r - 1, r - 2, (r - 1) // 2, (r + 1) // 2,
+          1 << 126, (1 << 127) - 1, 1 << 127, 1 << 128, (1 << 128) + lam, (2 * lam) % r, (3 * lam) % r]
+    ks += [(t * ((1 << 127) - 1) + lam * t) % r for t in range(1, 40)]
+    rng = random.Random(5)
+    ks += [rng.randrange(r) for _ in range(200)]
+    n = len(ks)
+    B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=7)
+    S = enc.scalars_array(ks)
+    exp = _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
+    assert svgpu.msm_arrays(B, S, svgpu.SV_CANONICAL) == exp
+    # each edge scalar alone (single-term MSMs) -- the split of every k is exercised in isolation
+    for k in ks[:19]:
+        Sk = enc.scalars_array([k])
+        assert svgpu.msm_arrays(B[:1], Sk) == _to_pt(oracle_cpp.msm_pippenger(B[:1], Sk, 0)), hex(k)

@@ -23,6 +23,7 @@
 #include <cstring>
 
 #include "curve.hpp"
+#include "glv.hpp"
 #include "msm_batch.hpp"
 #include "runtime.hpp"
 
@@ -69,9 +70,11 @@ __device__ __forceinline__ G1Xyzz smul_small(const G1Xyzz& p, uint32_t k) {
   return r;
 }
 
+// GLV (glv.hpp): every term k P is split into k1 P + k2 phi(P) with |k_i| < 2^127, so the windows
+// cover 128 bits and the per-MSM Horner chain is ~128 doublings instead of ~255.
 template <int C>
 struct BatchCfg {
-  static constexpr int W = (255 + C - 1) / C;  // signed digits of a < 2^254 scalar fit in 255 bits
+  static constexpr int W = (128 + C - 1) / C;  // signed digits of a < 2^127 half scalar
   static constexpr int B = 1 << (C - 1);
   static constexpr int G = B < 64 ? B : 64;  // lanes per window
   static constexpr int BPL = B / G;          // buckets per lane
@@ -89,11 +92,11 @@ __global__ void __launch_bounds__(kThreads) k_msm_batch_windows(const G1Aff* __r
                                                                  G1Xyzz* __restrict__ Tg, uint32_t* __restrict__ err) {
   using Cf = BatchCfg<C>;
   constexpr int W = Cf::W, B = Cf::B, G = Cf::G, BPL = Cf::BPL, WPB = Cf::WPB, NCH = Cf::NCH;
-  __shared__ uint32_t cur[WPB * B];   // histogram, then scatter cursors (= bucket ends)
-  __shared__ uint16_t bst[WPB * B];   // bucket starts within the window's list
-  __shared__ uint16_t dig[NCH * WPB]; // magnitude | sign << 8
-  __shared__ uint16_t lst[WPB * NCH]; // term index | sign << 15
-  __shared__ G1Xyzz T[WPB];           // window sums of this block's windows
+  __shared__ uint32_t cur[WPB * B];       // histogram, then scatter cursors (= bucket ends)
+  __shared__ uint16_t bst[WPB * B];       // bucket starts within the window's list
+  __shared__ uint16_t dig[2 * NCH * WPB]; // magnitude | sign << 8, per (half term, window)
+  __shared__ uint16_t lst[WPB * 2 * NCH]; // half-term index (term | half << 8) | sign << 15
+  __shared__ G1Xyzz T[WPB];               // window sums of this block's windows
 
   const int tid = threadIdx.x;
   const uint32_t id = ids ? ids[blockIdx.x] : blockIdx.x;  // optional indirection (host API skips big MSMs)
@@ -101,6 +104,7 @@ __global__ void __launch_bounds__(kThreads) k_msm_batch_windows(const G1Aff* __r
   const int nw = W - w0 < WPB ? W - w0 : WPB;
   const uint64_t b0 = off[id], e0 = off[id + 1];
   if (tid < WPB) T[tid] = G1Xyzz::identity();
+  const Fq beta = fq_const(GLV_BETA_MONT);
 
   for (uint64_t c0 = b0; c0 < e0; c0 += NCH) {
     const int m = (int)(e0 - c0 < (uint64_t)NCH ? e0 - c0 : (uint64_t)NCH);
@@ -115,28 +119,34 @@ __global__ void __launch_bounds__(kThreads) k_msm_batch_windows(const G1Aff* __r
       }
       if (!s.is_reduced()) atomicOr(err, 2u);
       if (mont) s = fe_from_mont(s);
-      // signed digits: the carry runs from window 0, only this block's windows are kept
-      uint32_t carry = 0;
-      for (int w = 0; w < w0 + nw; w++) {
-        const int pos = w * C, limb = pos >> 5, sh = pos & 31;
-        const uint32_t lo = limb < 8 ? s.v[limb] : 0u;
-        const uint32_t hi = limb + 1 < 8 ? s.v[limb + 1] : 0u;
-        uint32_t bits = sh ? ((lo >> sh) | (hi << (32 - sh))) : lo;
-        bits = (bits & ((1u << C) - 1)) + carry;
-        uint32_t mag, neg;
-        if (bits > (uint32_t)B) {  // digit bits - 2^C < 0 (bits == 2^C: digit 0, carry 1)
-          mag = (1u << C) - bits;
-          neg = mag ? 1u : 0u;
-          carry = 1;
-        } else {
-          mag = bits;
-          neg = 0;
-          carry = 0;
-        }
-        if (w >= w0) {
-          const int lw = w - w0;
-          dig[tid * WPB + lw] = (uint16_t)(mag | (neg << 8));
-          if (mag) atomicAdd(&cur[lw * B + mag - 1], 1u);
+      uint32_t hv[2][4];
+      glv_split(s.v, hv[0], hv[1]);
+      for (int h = 0; h < 2; h++) {
+        const uint32_t sg = hv[h][3] >> 31;
+        hv[h][3] &= 0x7fffffffu;
+        // signed digits: the carry runs from window 0, only this block's windows are kept
+        uint32_t carry = 0;
+        for (int w = 0; w < w0 + nw; w++) {
+          const int pos = w * C, limb = pos >> 5, sh = pos & 31;
+          const uint32_t lo = limb < 4 ? hv[h][limb] : 0u;
+          const uint32_t hi = limb + 1 < 4 ? hv[h][limb + 1] : 0u;
+          uint32_t bits = sh ? ((lo >> sh) | (hi << (32 - sh))) : lo;
+          bits = (bits & ((1u << C) - 1)) + carry;
+          uint32_t mag, neg;
+          if (bits > (uint32_t)B) {  // digit bits - 2^C < 0 (bits == 2^C: digit 0, carry 1)
+            mag = (1u << C) - bits;
+            neg = mag ? 1u : 0u;
+            carry = 1;
+          } else {
+            mag = bits;
+            neg = 0;
+            carry = 0;
+          }
+          if (w >= w0) {
+            const int lw = w - w0;
+            dig[(h * NCH + tid) * WPB + lw] = (uint16_t)(mag | ((neg ^ sg) << 8));
+            if (mag) atomicAdd(&cur[lw * B + mag - 1], 1u);
+          }
         }
       }
     }
@@ -152,14 +162,15 @@ __global__ void __launch_bounds__(kThreads) k_msm_batch_windows(const G1Aff* __r
     }
     __syncthreads();
     if (tid < m) {
-      for (int lw = 0; lw < nw; lw++) {
-        const uint32_t d = dig[tid * WPB + lw];
-        const uint32_t mag = d & 0xff;
-        if (mag) {
-          const uint32_t pos = atomicAdd(&cur[lw * B + mag - 1], 1u);
-          lst[lw * NCH + pos] = (uint16_t)(tid | ((d >> 8) << 15));
+      for (int h = 0; h < 2; h++)
+        for (int lw = 0; lw < nw; lw++) {
+          const uint32_t d = dig[(h * NCH + tid) * WPB + lw];
+          const uint32_t mag = d & 0xff;
+          if (mag) {
+            const uint32_t pos = atomicAdd(&cur[lw * B + mag - 1], 1u);
+            lst[lw * 2 * NCH + pos] = (uint16_t)(tid | (h << 8) | ((d >> 8) << 15));
+          }
         }
-      }
     }
     __syncthreads();
     {
@@ -172,14 +183,15 @@ __global__ void __launch_bounds__(kThreads) k_msm_batch_windows(const G1Aff* __r
           G1Xyzz acc = G1Xyzz::identity();
           const uint32_t pe = cur[lw * B + b];
           for (uint32_t p = bst[lw * B + b]; p < pe; p++) {
-            const uint32_t e = lst[lw * NCH + p];
-            const uint32_t* bp = reinterpret_cast<const uint32_t*>(bases + c0 + (e & 0x7fff));
+            const uint32_t e = lst[lw * 2 * NCH + p];
+            const uint32_t* bp = reinterpret_cast<const uint32_t*>(bases + c0 + (e & 0xff));
             Fq x = ld_fq(bp), y = ld_fq(bp + 8);
             if (x.is_zero() && y.is_zero()) continue;  // identity base
             if (!mont) {
               x = fe_to_mont(x);
               y = fe_to_mont(y);
             }
+            if ((e >> 8) & 1) x = x * beta;  // phi(P) = (beta x, y)
             if (e >> 15) y = -y;
             acc = xyzz_madd(acc, x, y);
           }

@@ -18,7 +18,7 @@
 //                     directly, bucket pieces that cross a thread boundary to pfirst/plast
 //   k_fixup           per bucket: join the pieces of buckets that cross thread boundaries
 //   k_wsum            bucket reduction, step 1: F_w = sum_b (b+1) S_b = sum_j acc_j + L sum_j j T_j
-//                     with running sums over segments of L = 4 buckets (acc_j, T_j per segment)
+//                     with running sums over segments of L = 8 buckets (acc_j, T_j per segment)
 //   k_group_sum       step 2: sum_j j T_j = sum_k 2^k U_k, U_k = sum_{j : bit k of j} T_j; the
 //                     subset sums U_k and the plain sum of acc_j are independent, so each is one
 //                     block-level tree reduction in LDS (low serial depth: the tail is latency-bound)
@@ -41,8 +41,6 @@
 namespace sv {
 
 static constexpr int kBlock = 256;
-static constexpr uint32_t kRedL = 4;  // buckets per thread in the running-sum level
-static constexpr int kRedLog = 2;
 
 __device__ __forceinline__ G1Aff load_aff(const G1Aff* __restrict__ a, uint32_t i) {
   const uint4* p = reinterpret_cast<const uint4*>(a + i);
@@ -463,16 +461,16 @@ __global__ void __launch_bounds__(kBlock) k_fixup_heavy(const uint32_t* __restri
   }
 }
 
-// One bucket-reduction level over `groups` groups of N elements, segments of L = kRedL:
+// One bucket-reduction level over `groups` groups of N elements, segments of L buckets:
 //   acc[g][j] = sum_{i in seg j} (i - jL + base) X[g][i],  tot[g][j] = sum_{i in seg j} X[g][i]
-__global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, uint32_t N, uint32_t J, uint32_t groups, int base,
+__global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, uint32_t N, uint32_t J, uint32_t L, uint32_t groups, int base,
                        G1Xyzz* __restrict__ acc_out, G1Xyzz* __restrict__ tot_out) {
   uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= J * groups) return;
   uint32_t g = tid / J, j = tid % J;
   const G1Xyzz* x = X + (size_t)g * N;
-  uint32_t lo = j * kRedL;
-  uint32_t hi = min(N, lo + kRedL);
+  uint32_t lo = j * L;
+  uint32_t hi = min(N, lo + L);
   G1Xyzz run = G1Xyzz::identity(), acc = G1Xyzz::identity();
   for (uint32_t i = hi; i-- > lo;) {
     run = xyzz_add(run, load_xyzz(x, i));
@@ -549,7 +547,11 @@ MsmPlan msm_plan(size_t n) {
   p.K = (uint32_t)K;
   p.T = cdiv(entries, p.K);
   // reduction: J running-sum segments per window, NG subset groups of H = J/2 points
-  p.J = p.B / kRedL;
+  p.logL = 3;  // 8 buckets per running-sum segment (swept: tools/gpu_sweep_red.sh)
+  if (const char* e = getenv("SVGPU_RED_LOG")) p.logL = atoi(e);
+  if (p.logL < 1) p.logL = 1;
+  if (p.logL > p.c - 3) p.logL = p.c - 3 > 1 ? p.c - 3 : 1;
+  p.J = p.B >> p.logL;
   p.logJ = 0;
   while ((1u << p.logJ) < p.J) p.logJ++;
   p.NG = 2 + p.logJ;
@@ -594,11 +596,11 @@ MsmPlan msm_plan(size_t n) {
 
 // Host Horner over (window, group) terms: total = sum_w 2^(c w) [A_lo + A_hi + sum_k 2^(2+k) U_k].
 static host::Xyzz host_combine(const MsmPlan& p, const host::Xyzz* A /* [W][NG] */) {
-  int maxe = (int)(p.c * (p.W - 1) + kRedLog + p.logJ);
+  int maxe = (int)(p.c * (p.W - 1) + p.logL + p.logJ);
   std::vector<host::Xyzz> byexp(maxe + 1, host::x_identity());
   for (uint32_t w = 0; w < p.W; w++)
     for (uint32_t q = 0; q < p.NG; q++) {
-      int e = (int)(p.c * w + (q < 2 ? 0 : kRedLog + (q - 2)));
+      int e = (int)(p.c * w + (q < 2 ? 0 : p.logL + (q - 2)));
       byexp[e] = host::x_add(byexp[e], A[w * p.NG + q]);
     }
   host::Xyzz acc = host::x_identity();
@@ -705,9 +707,9 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
   hipLaunchKernelGGL(k_fixup_heavy, dim3(256), dim3(kBlock), 0, st, gst, p.K, pfirst, plast, heavy, nheavy,
                      bsum);
   SV_HIP(hipEventRecord(ev[4], st));
-  // bucket reduction: running sums over segments of kRedL buckets, then the subset sums
+  // bucket reduction: running sums over segments of 2^logL buckets, then the subset sums
   hipLaunchKernelGGL(k_wsum, dim3(cdiv((uint64_t)p.J * p.W, kBlock)), dim3(kBlock), 0, st, bsum, p.B, p.J,
-                     p.W, 1, racc, rtot);
+                     1u << p.logL, p.W, 1, racc, rtot);
   hipLaunchKernelGGL(k_group_sum, dim3(p.NG * p.W), dim3(kGroupBlock), 0, st, racc, rtot, p.J, p.logJ, ping);
   SV_HIP(hipGetLastError());
   SV_HIP(hipEventRecord(ev[5], st));

@@ -17,7 +17,8 @@ struct MsmPlan {
   uint32_t nbt;     // W * B
   uint32_t K;       // sorted entries per accumulate thread
   uint32_t T;       // accumulate threads
-  uint32_t J;       // running-sum segments per window (B / 4)
+  uint32_t logL;    // log2 of the buckets per running-sum segment
+  uint32_t J;       // running-sum segments per window (B >> logL)
   uint32_t logJ;    // log2(J)
   uint32_t NG;      // subset-sum groups per window: 2 + logJ
 };

@@ -374,6 +374,70 @@ __device__ __forceinline__ void eval_lines(LineCoeff* __restrict__ E, const Line
   }
 }
 
+// ---- Step multipliers (S = 8 path): the Miller loop's line products are known once the lines are
+// evaluated, so the prologue folds them off the critical path.  Pair idx (the lines of both G2
+// points at one step) becomes the 5-sparse D_idx = (a0 + a1 w + a3 w^3)(b0 + b1 w + b3 w^3), and a
+// step with an addition (or the final Frobenius steps) multiplies its two pairs into a dense M.
+// The loop then costs one square and ONE multiplication per step (66) instead of a square and
+// 2-4 sparse line steps (176).
+struct MergeTab {
+  int8_t first[32];  // first pair index of each merged step (the second is first + 1)
+  int n;
+};
+constexpr MergeTab make_merges() {
+  MergeTab t{};
+  int idx = 0, m = 0;
+  for (int i = ATE_NAF_LEN - 1; i >= 1; i--) {
+    if (ATE_NAF[i - 1] != 0) {
+      t.first[m++] = (int8_t)idx;
+      idx += 2;
+    } else {
+      idx += 1;
+    }
+  }
+  t.first[m++] = (int8_t)idx;  // the two Frobenius steps
+  t.n = m;
+  return t;
+}
+__constant__ MergeTab c_merge = make_merges();
+static constexpr int kMaxMerge = 32;
+
+// D_idx for pairs idx = lane, lane + lanes, ...: 6 Fq2 products (Karatsuba on the three cross terms)
+__device__ __forceinline__ void pair_products(Fq2* __restrict__ D, const LineCoeff* __restrict__ E, int lane,
+                                              int lanes) {
+  for (int idx = lane; idx < ATE_NUM_LINES; idx += lanes) {
+    const LineCoeff A = E[2 * idx], Bq = E[2 * idx + 1];
+    const Fq2 m00 = A.c0 * Bq.c0, m11 = A.c3 * Bq.c3, m33 = A.c4 * Bq.c4;
+    const Fq2 x01 = (A.c0 + A.c3) * (Bq.c0 + Bq.c3);
+    const Fq2 x03 = (A.c0 + A.c4) * (Bq.c0 + Bq.c4);
+    const Fq2 x13 = (A.c3 + A.c4) * (Bq.c3 + Bq.c4);
+    Fq2* d = D + 6 * idx;
+    d[0] = m00 + fq2_mul_xi(m33);
+    d[1] = x01 - m00 - m11;
+    d[2] = m11;
+    d[3] = x03 - m00 - m33;
+    d[4] = x13 - m11 - m33;
+    d[5] = Fq2::zero();
+  }
+}
+
+// M_m = D_a D_{a+1} (both 5-sparse) for every merged step; job = (step, output coefficient)
+__device__ __forceinline__ void merge_products(Fq2* __restrict__ M, const Fq2* __restrict__ D, int lane, int lanes) {
+  for (int job = lane; job < c_merge.n * 6; job += lanes) {
+    const int m = job / 6, k = job % 6;
+    const Fq2* a = D + 6 * c_merge.first[m];
+    const Fq2* b = a + 6;
+    Fq2 lo = Fq2::zero(), hi = Fq2::zero();
+    for (int i = 0; i < 5; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < 5) lo = lo + a[i] * b[j];
+      const int jw = k + 6 - i;
+      if (jw >= 0 && jw < 5) hi = hi + a[i] * b[jw];
+    }
+    M[6 * m + k] = lo + fq2_mul_xi(hi);
+  }
+}
+
 template <int S>
 __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ lhs, const G1Aff* __restrict__ rhs,
                                                       uint32_t n, const LineCoeff* __restrict__ L1,
@@ -385,6 +449,8 @@ __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ l
   __shared__ Fq2 sh[2 * NGRP * 6];
   __shared__ LineCoeff ev[NGRP][2 * ATE_NUM_LINES];
   __shared__ Fq2 tabk[NGRP][(kTab + kKeep) * 6];
+  constexpr bool kMerged = S == 8;  // one group per wave: room for the step multipliers in LDS
+  __shared__ Fq2 dmul[kMerged ? ATE_NUM_LINES * 6 : 1];
   const int lane = threadIdx.x, grp = lane / GL, gl = lane % GL;
   const bool active = gl < 6 * S;
   const int k = active ? gl / S : 5, sub = active ? gl % S : 0;
@@ -407,21 +473,38 @@ __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ l
   const LineCoeff* E = ev[grp];
   Fq2 f = G.k == 0 ? Fq2::one() : Fq2::zero();
   int idx = 0;
-  for (int i = ATE_NAF_LEN - 1; i >= 1 && (phases & 1); i--) {
-    if (i != ATE_NAF_LEN - 1) f = g_msq<S>(G, f);
-    f = g_mline<S>(G, f, E[2 * idx].c0, E[2 * idx].c3, E[2 * idx].c4);
-    f = g_mline<S>(G, f, E[2 * idx + 1].c0, E[2 * idx + 1].c3, E[2 * idx + 1].c4);
-    idx++;
-    if (c_naf[i - 1] != 0) {
+  if constexpr (kMerged) {
+    pair_products(dmul, E, gl, GL);
+    __syncthreads();
+    Fq2* M = reinterpret_cast<Fq2*>(ev[grp]);  // the evaluated lines are dead now
+    static_assert(sizeof(ev[0]) >= kMaxMerge * 6 * sizeof(Fq2), "merged steps must fit the line buffer");
+    merge_products(M, dmul, gl, GL);
+    __syncthreads();
+    int m = 0;
+    for (int i = ATE_NAF_LEN - 1; i >= 1 && (phases & 1); i--) {
+      const Fq2* mul = c_naf[i - 1] != 0 ? M + 6 * m++ : dmul + 6 * idx;
+      idx += c_naf[i - 1] != 0 ? 2 : 1;
+      if (i == ATE_NAF_LEN - 1) f = mul[G.k];  // f = 1 * mul
+      else f = g_mul_lds<S>(G, g_msq<S>(G, f), mul);
+    }
+    if (phases & 1) f = g_mul_lds<S>(G, f, M + 6 * m);  // the two Frobenius steps
+  } else {
+    for (int i = ATE_NAF_LEN - 1; i >= 1 && (phases & 1); i--) {
+      if (i != ATE_NAF_LEN - 1) f = g_msq<S>(G, f);
+      f = g_mline<S>(G, f, E[2 * idx].c0, E[2 * idx].c3, E[2 * idx].c4);
+      f = g_mline<S>(G, f, E[2 * idx + 1].c0, E[2 * idx + 1].c3, E[2 * idx + 1].c4);
+      idx++;
+      if (c_naf[i - 1] != 0) {
+        f = g_mline<S>(G, f, E[2 * idx].c0, E[2 * idx].c3, E[2 * idx].c4);
+        f = g_mline<S>(G, f, E[2 * idx + 1].c0, E[2 * idx + 1].c3, E[2 * idx + 1].c4);
+        idx++;
+      }
+    }
+    for (int st = 0; st < 2 && (phases & 1); st++) {
       f = g_mline<S>(G, f, E[2 * idx].c0, E[2 * idx].c3, E[2 * idx].c4);
       f = g_mline<S>(G, f, E[2 * idx + 1].c0, E[2 * idx + 1].c3, E[2 * idx + 1].c4);
       idx++;
     }
-  }
-  for (int st = 0; st < 2 && (phases & 1); st++) {
-    f = g_mline<S>(G, f, E[2 * idx].c0, E[2 * idx].c3, E[2 * idx].c4);
-    f = g_mline<S>(G, f, E[2 * idx + 1].c0, E[2 * idx + 1].c3, E[2 * idx + 1].c4);
-    idx++;
   }
   // final exponentiation (same chain as curve.hpp final_exponentiation)
   // (phases: debug/profiling knob SVGPU_DECIDER_PHASES, 3 = both halves; results are only valid at 3)

@@ -16,7 +16,9 @@
 //   k_accumulate      each thread sums K consecutive sorted entries (mixed XYZZ adds; perfect
 //                     load balance whatever the digit distribution), complete buckets written
 //                     directly, bucket pieces that cross a thread boundary to pfirst/plast
-//   k_fixup           per bucket: join the pieces of buckets that cross thread boundaries
+//                     (two-piece buckets inside a block are joined at the end through LDS)
+//   k_fixup_multi     the other crossing buckets, queued by k_accumulate (k_fixup_heavy: block-level
+//                     tree for buckets spanning more than 9 threads)
 //   k_wsum            bucket reduction, step 1: F_w = sum_b (b+1) S_b = sum_j acc_j + L sum_j j T_j
 //                     with running sums over segments of L = 8 buckets (acc_j, T_j per segment)
 //   k_group_sum       step 2: sum_j j T_j = sum_k 2^k U_k, U_k = sum_{j : bit k of j} T_j; the
@@ -34,6 +36,7 @@
 #include <vector>
 
 #include "curve.hpp"
+#include "glv.hpp"
 #include "host_ec.hpp"
 #include "msm.hpp"
 #include "runtime.hpp"
@@ -92,11 +95,14 @@ __global__ void k_to_mont_bases(const G1Aff* __restrict__ in, G1Aff* __restrict_
   reinterpret_cast<uint4*>(out + i)[3] = make_uint4(r.y.v[4], r.y.v[5], r.y.v[6], r.y.v[7]);
 }
 
-// Signed windows: digit_w = bits[cw, cw+c) + carry, mapped to (-2^(c-1), 2^(c-1)].  W = ceil(255/c)
-// windows so the top digit never carries out (scalars < r < 2^254).  f(w, mag, neg) per window.
-template <int C, class F>
+// Signed windows: digit_w = bits[cw, cw+c) + carry, mapped to (-2^(c-1), 2^(c-1)].  W = ceil(NB/c)
+// windows so the top digit never carries out: NB = 255 for full scalars (< r < 2^254), NB = 128 for
+// GLV halves (magnitude < 2^127).  f(w, mag, neg) per window.
+template <int C, int NB>
+__host__ __device__ constexpr int num_windows() { return (NB + C - 1) / C; }
+template <int C, int NB = 255, class F>
 __device__ __forceinline__ void for_each_digit(const Fr& s, F&& f) {
-  constexpr int W = (255 + C - 1) / C;
+  constexpr int W = num_windows<C, NB>();
   uint32_t carry = 0;
   const uint32_t half = 1u << (C - 1);
   const uint32_t mask = (1u << C) - 1;
@@ -130,6 +136,52 @@ __device__ __forceinline__ Fr load_scalar(const Fr* __restrict__ scalars, uint32
   return mont_in ? fe_from_mont(s) : s;
 }
 
+// Scalar of virtual point i for the sort passes: a full scalar (NB = 255), or a GLV half (NB = 128,
+// glv_pack layout: 127-bit magnitude, sign in bit 31 of limb 3 -> sgn, folded into every digit).
+template <int NB>
+__device__ __forceinline__ Fr load_digits_src(const void* __restrict__ src, uint32_t i, int mont_in,
+                                              uint32_t* __restrict__ err, uint32_t& sgn) {
+  if constexpr (NB == 255) {
+    sgn = 0;
+    return load_scalar(reinterpret_cast<const Fr*>(src), i, mont_in, err);
+  } else {
+    const uint4 q = reinterpret_cast<const uint4*>(src)[i];
+    Fr s;
+    s.v[0] = q.x; s.v[1] = q.y; s.v[2] = q.z; s.v[3] = q.w & 0x7fffffffu;
+    s.v[4] = 0; s.v[5] = 0; s.v[6] = 0; s.v[7] = 0;
+    sgn = q.w >> 31;
+    return s;
+  }
+}
+
+// GLV preparation (glv.hpp): scalar k_i -> halves (k1, k2) stored as hs[i], hs[n + i]; the
+// endomorphism image phi(P_i) = (beta x_i, y_i) stored as phi[i] (identity (0, 0) maps to itself).
+// The sort and accumulate passes then run over 2n virtual points with 128-bit scalars.
+__global__ void k_glv_prep(const G1Aff* __restrict__ bases, const Fr* __restrict__ scalars, uint32_t n,
+                           int mont_in, uint4* __restrict__ hs, G1Aff* __restrict__ phi,
+                           uint32_t* __restrict__ err) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Fr k = load_scalar(scalars, i, mont_in, err);
+  uint32_t h1[4], h2[4];
+  glv_split(k.v, h1, h2);
+  hs[i] = make_uint4(h1[0], h1[1], h1[2], h1[3]);
+  hs[n + i] = make_uint4(h2[0], h2[1], h2[2], h2[3]);
+  const uint4* b = reinterpret_cast<const uint4*>(bases + i);
+  Fq x, beta;
+  const uint4 x0 = b[0], x1 = b[1];
+  x.v[0] = x0.x; x.v[1] = x0.y; x.v[2] = x0.z; x.v[3] = x0.w;
+  x.v[4] = x1.x; x.v[5] = x1.y; x.v[6] = x1.z; x.v[7] = x1.w;
+#pragma unroll
+  for (int j = 0; j < 8; j++) beta.v[j] = GLV_BETA_MONT[j];
+  const Fq bx = x * beta;
+  uint4* o = reinterpret_cast<uint4*>(phi + i);
+  o[0] = make_uint4(bx.v[0], bx.v[1], bx.v[2], bx.v[3]);
+  o[1] = make_uint4(bx.v[4], bx.v[5], bx.v[6], bx.v[7]);
+  o[2] = b[2];
+  o[3] = b[3];
+}
+
 // ---- two-level counting sort of the n * W (point, digit) entries by bucket ------------------
 // Bucket b = |digit| - 1 of window w splits into a coarse bin b >> FB (NBIN = 2^CB bins per window)
 // and a fine index b & (2^FB - 1).  Pass 1 (k_bin_hist): per block of sort_chunk(c) points, every
@@ -142,7 +194,10 @@ __device__ __forceinline__ Fr load_scalar(const Fr* __restrict__ scalars, uint32
 // accumulate chunk [tK, tK + K).  No per-(window, point) digit array is ever stored.
 // points per block in passes 1 and 3: 512 (2 per thread), 256 when the LDS staging of W digits
 // per point would not fit (small c, many windows)
-__host__ __device__ constexpr uint32_t sort_chunk(int c) { return (255 + c - 1) / c > 20 ? 256u : 512u; }
+__host__ __device__ constexpr uint32_t sort_chunk(int c, int nb = 255) { return (nb + c - 1) / c > 20 ? 256u : 512u; }
+// coarse bits: 2^CB bins per window, so that W * 2^CB ~ 1024 fine-sort regions of ~16K entries at
+// 2^20 (LDS-staged in k_fine_sort) -- 64 bins for the 16 full-width windows, 128 for the 8 GLV ones
+__host__ __device__ constexpr int coarse_bits(int c, int nb) { return c - 1 < (nb == 128 ? 7 : 6) ? c - 1 : (nb == 128 ? 7 : 6); }
 
 // exclusive scan of x[0 .. N) in LDS by a 256-thread block (N <= 4096); returns the total
 template <int N>
@@ -177,20 +232,21 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t* x, uint32_t* part)
   return total;
 }
 
-template <int C>
-__global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scalars, uint32_t n, int mont_in,
+template <int C, int NB>
+__global__ void __launch_bounds__(kBlock) k_bin_hist(const void* __restrict__ scalars, uint32_t n, int mont_in,
                                                      uint32_t nblk, uint32_t* __restrict__ bcnt,
                                                      uint32_t* __restrict__ err) {
-  constexpr int W = (255 + C - 1) / C, LOGB = C - 1;
-  constexpr int CB = LOGB < 6 ? LOGB : 6, FB = LOGB - CB, NBIN = 1 << CB;
+  constexpr int W = num_windows<C, NB>(), LOGB = C - 1;
+  constexpr int CB = coarse_bits(C, NB), FB = LOGB - CB, NBIN = 1 << CB;
   __shared__ uint32_t h[W * NBIN];
   for (int k = threadIdx.x; k < W * NBIN; k += kBlock) h[k] = 0;
   __syncthreads();
-  constexpr uint32_t CH = sort_chunk(C);
+  constexpr uint32_t CH = sort_chunk(C, NB);
   const uint32_t lo = blockIdx.x * CH, hi = min(n, lo + CH);
   for (uint32_t i = lo + threadIdx.x; i < hi; i += kBlock) {
-    const Fr s = load_scalar(scalars, i, mont_in, err);
-    for_each_digit<C>(s, [&](int w, uint32_t mag, uint32_t) {
+    uint32_t sgn;
+    const Fr s = load_digits_src<NB>(scalars, i, mont_in, err, sgn);
+    for_each_digit<C, NB>(s, [&](int w, uint32_t mag, uint32_t) {
       if (mag) atomicAdd(&h[w * NBIN + ((mag - 1) >> FB)], 1u);
     });
   }
@@ -252,15 +308,15 @@ __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __restrict__ 
 
 // Pass 3: the block's entries are first placed in LDS grouped by (window, bin), then each group
 // is copied to its global run with consecutive lanes writing consecutive addresses.
-template <int C>
-__global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ scalars, uint32_t n, int mont_in,
+template <int C, int NB>
+__global__ void __launch_bounds__(kBlock) k_bin_scatter(const void* __restrict__ scalars, uint32_t n, int mont_in,
                                                         uint32_t nblk, const uint32_t* __restrict__ bcnt,
                                                         const uint32_t* __restrict__ bstart,
                                                         uint64_t* __restrict__ tmp) {
-  constexpr int W = (255 + C - 1) / C, LOGB = C - 1;
-  constexpr int CB = LOGB < 6 ? LOGB : 6, FB = LOGB - CB, NBIN = 1 << CB, NK = W * NBIN;
+  constexpr int W = num_windows<C, NB>(), LOGB = C - 1;
+  constexpr int CB = coarse_bits(C, NB), FB = LOGB - CB, NBIN = 1 << CB, NK = W * NBIN;
   constexpr uint32_t FMASK = (1u << FB) - 1;
-  constexpr uint32_t CH = sort_chunk(C), PT = CH / kBlock;
+  constexpr uint32_t CH = sort_chunk(C, NB), PT = CH / kBlock;
   __shared__ uint32_t off[NK];   // local group offsets
   __shared__ uint32_t cur[NK];   // cursors
   __shared__ uint32_t part[kBlock];
@@ -270,12 +326,13 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
   for (int k = threadIdx.x; k < NK; k += kBlock) off[k] = 0;
   __syncthreads();
   Fr sc[PT];
+  uint32_t sg[PT];
 #pragma unroll
   for (int j = 0; j < (int)PT; j++) {
     const uint32_t i = lo + threadIdx.x + j * kBlock;
     if (i < hi) {
-      sc[j] = load_scalar(scalars, i, mont_in, nullptr);
-      for_each_digit<C>(sc[j], [&](int w, uint32_t mag, uint32_t) {
+      sc[j] = load_digits_src<NB>(scalars, i, mont_in, nullptr, sg[j]);
+      for_each_digit<C, NB>(sc[j], [&](int w, uint32_t mag, uint32_t) {
         if (mag) atomicAdd(&off[w * NBIN + ((mag - 1) >> FB)], 1u);
       });
     }
@@ -288,12 +345,12 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
   for (int j = 0; j < (int)PT; j++) {
     const uint32_t li = threadIdx.x + j * kBlock;
     if (lo + li < hi) {
-      for_each_digit<C>(sc[j], [&](int w, uint32_t mag, uint32_t neg) {
+      for_each_digit<C, NB>(sc[j], [&](int w, uint32_t mag, uint32_t neg) {
         if (mag) {
           const uint32_t b = mag - 1;
           const uint32_t k = w * NBIN + (b >> FB);
           const uint32_t pos = atomicAdd(&cur[k], 1u);
-          stage[pos] = li | (neg << 9) | ((b & FMASK) << 10);
+          stage[pos] = li | ((neg ^ sg[j]) << 9) | ((b & FMASK) << 10);
           key[pos] = (uint16_t)k;
         }
       });
@@ -309,18 +366,39 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
   }
 }
 
-// one block per (window, bin): counting sort by the fine index within the bin's region
+// one block per (window, bin): counting sort by the fine index within the bin's region.
+// Regions of up to kFineCap entries (every bin but the short top window's at n = 2^20) are read
+// from tmp ONCE into registers and sorted into an LDS copy of the region, which is then written to
+// ent[] with consecutive lanes on consecutive addresses: the direct scatter of 4-byte entries to
+// global memory cost ~5x its bytes in partial-line write traffic (PMC WRITE_SIZE, r01).  Larger
+// regions take the two-read global-scatter path.
+static constexpr uint32_t kFineR = 18;                 // entries per thread held in registers
+static constexpr uint32_t kFineCap = 1024 * kFineR;    // region entries staged in LDS
+static constexpr size_t kFineLds = (512 + 1024 + (size_t)kFineCap) * 4;  // 78 KiB: 2 blocks per CU
 __global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__ tmp,
                                                     const uint32_t* __restrict__ bstart, uint32_t FB, uint32_t K,
                                                     uint32_t* __restrict__ gst, uint32_t* __restrict__ tstart,
                                                     uint32_t* __restrict__ ent) {
-  __shared__ uint32_t fc[512];
-  __shared__ uint32_t part[1024];
+  extern __shared__ __attribute__((aligned(16))) uint32_t fine_lds[];
+  uint32_t* fc = fine_lds;           // [512] fine-bucket counters / cursors
+  uint32_t* part = fine_lds + 512;   // [1024] scan partials
+  uint32_t* out = fine_lds + 1536;   // [kFineCap] the sorted region
   const uint32_t wb = blockIdx.x, tid = threadIdx.x, NF = 1u << FB;
-  const uint32_t s0 = bstart[wb], s1 = bstart[wb + 1];
+  const uint32_t s0 = bstart[wb], s1 = bstart[wb + 1], len = s1 - s0;
+  const bool staged = len <= kFineCap;  // block-uniform
   for (uint32_t f = tid; f < NF; f += 1024) fc[f] = 0;
   __syncthreads();
-  {
+  uint64_t x[kFineR];
+  if (staged) {
+#pragma unroll
+    for (uint32_t r = 0; r < kFineR; r++) {
+      const uint32_t i = tid + r * 1024;
+      x[r] = i < len ? tmp[s0 + i] : 0;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kFineR; r++)
+      if (tid + r * 1024 < len) atomicAdd(&fc[(uint32_t)(x[r] >> 32)], 1u);
+  } else {
     uint32_t e = s0 + tid;
     for (; e + 3 * 1024 < s1; e += 4 * 1024) {  // 4 loads in flight per thread
       const uint32_t f0 = (uint32_t)(tmp[e] >> 32), f1 = (uint32_t)(tmp[e + 1024] >> 32);
@@ -347,88 +425,135 @@ __global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__
     const uint32_t st = s0 + part[tid] - v, en = st + v;
     const uint32_t g = wb * NF + tid;  // global bucket = w * B + b
     gst[g] = st;
-    fc[tid] = st;
+    fc[tid] = staged ? st - s0 : st;
     for (uint32_t t = (st + K - 1) / K; t * K < en; t++) tstart[t] = g;
   }
   __syncthreads();
+  if (staged) {
+#pragma unroll
+    for (uint32_t r = 0; r < kFineR; r++)
+      if (tid + r * 1024 < len) out[atomicAdd(&fc[(uint32_t)(x[r] >> 32)], 1u)] = (uint32_t)x[r];
+    __syncthreads();
+    for (uint32_t i = tid; i < len; i += 1024) ent[s0 + i] = out[i];
+    return;
+  }
   uint32_t e = s0 + tid;
   for (; e + 3 * 1024 < s1; e += 4 * 1024) {
-    uint64_t x[4];
+    uint64_t y[4];
 #pragma unroll
-    for (int j = 0; j < 4; j++) x[j] = tmp[e + j * 1024];
+    for (int j = 0; j < 4; j++) y[j] = tmp[e + j * 1024];
 #pragma unroll
-    for (int j = 0; j < 4; j++) ent[atomicAdd(&fc[(uint32_t)(x[j] >> 32)], 1u)] = (uint32_t)x[j];
+    for (int j = 0; j < 4; j++) ent[atomicAdd(&fc[(uint32_t)(y[j] >> 32)], 1u)] = (uint32_t)y[j];
   }
   for (; e < s1; e += 1024) {
-    const uint64_t x = tmp[e];
-    ent[atomicAdd(&fc[(uint32_t)(x >> 32)], 1u)] = (uint32_t)x;
+    const uint64_t y = tmp[e];
+    ent[atomicAdd(&fc[(uint32_t)(y >> 32)], 1u)] = (uint32_t)y;
   }
 }
 
 // Each thread: K consecutive sorted entries.  See file header.
+// Bucket pieces: a bucket whose entries cross thread boundaries is split into an OWNER piece (the
+// thread holding its first entry; always that thread's last segment) and HEAD pieces (a later
+// thread's first segment).  A bucket of exactly two pieces inside one block -- nearly all of them
+// for random scalars -- is joined here: the head goes to LDS, and after the barrier the owner adds
+// it to the piece still in its registers (one extra addition per owner at the accumulate's full
+// occupancy, no global round trip).  Every other crossing bucket keeps the global pieces
+// (pfirst = a thread's first segment, plast = its last) and is queued for k_fixup_multi.  Empty
+// buckets are never written: k_wsum reads gst.
+__device__ __forceinline__ bool join_in_block(uint32_t gs, uint32_t ge, uint32_t K) {
+  const uint32_t t0 = gs / K, t1 = (ge - 1) / K;
+  return t1 == t0 + 1 && t0 / kBlock == t1 / kBlock;
+}
 __global__ void __launch_bounds__(kBlock) k_accumulate(
     const G1Aff* __restrict__ bases, const uint32_t* __restrict__ ent, const uint32_t* __restrict__ gst,
     const uint32_t* __restrict__ tstart, uint32_t nbt, uint32_t K, uint32_t T,
-    G1Xyzz* __restrict__ bsum, G1Xyzz* __restrict__ pfirst, G1Xyzz* __restrict__ plast) {
-  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= T) return;
+    G1Xyzz* __restrict__ bsum, G1Xyzz* __restrict__ pfirst, G1Xyzz* __restrict__ plast,
+    uint32_t* __restrict__ multi, uint32_t* __restrict__ nmulti, const G1Aff* __restrict__ phi,
+    uint32_t nsplit) {
+  __shared__ G1Xyzz shead[kBlock];
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t m = gst[nbt];
   const uint32_t s0 = t * K;
-  if (s0 >= m) return;
-  const uint32_t e_end = min(s0 + K, m);
-  uint32_t g = tstart[t];
-  uint32_t gs = gst[g], ge = gst[g + 1];
-  uint32_t seg_start = s0;
-  bool first = true;
+  const bool active = t < T && s0 < m;
+  // owner piece left in acc for the in-block join (g = its bucket), or none
+  bool owner = false;
+  uint32_t g = 0, gs = 0, ge = 0;
   G1Xyzz acc = G1Xyzz::identity();
-  for (uint32_t e = s0; e < e_end; e++) {
-    if (e >= ge) {
-      if (seg_start == gs && e == ge) store_xyzz(bsum, g, acc);
-      else if (first) store_xyzz(pfirst, t, acc);
-      else store_xyzz(plast, t, acc);
-      first = false;
-      do {
-        g++;
-        gs = ge;
-        ge = gst[g + 1];
-      } while (ge <= e);
-      seg_start = e;
-      acc = G1Xyzz::identity();
+  if (active) {
+    const uint32_t e_end = min(s0 + K, m);
+    g = tstart[t];
+    gs = gst[g];
+    ge = gst[g + 1];
+    uint32_t seg_start = s0;
+    bool first = true;
+    for (uint32_t e = s0; e < e_end; e++) {
+      if (e >= ge) {  // segment [seg_start, ge) of bucket g ends inside this chunk
+        if (seg_start == gs) {
+          store_xyzz(bsum, g, acc);
+        } else {  // head piece of a bucket owned by an earlier thread
+          if (join_in_block(gs, ge, K)) shead[threadIdx.x] = acc;
+          else store_xyzz(pfirst, t, acc);
+        }
+        first = false;
+        do {
+          g++;
+          gs = ge;
+          ge = gst[g + 1];
+        } while (ge <= e);
+        seg_start = e;
+        acc = G1Xyzz::identity();
+      }
+      const uint32_t v = ent[e], idx = v & 0x7fffffffu;
+      // virtual point idx: P_idx, or phi(P_(idx - n)) for the GLV halves (nsplit = n; ~0u without GLV)
+      G1Aff p = load_aff(idx >= nsplit ? phi + (idx - nsplit) : bases + idx, 0);
+      if (v & 0x80000000u) p.y = -p.y;
+      acc = xyzz_madd_aff(acc, p);
     }
-    uint32_t v = ent[e];
-    G1Aff p = load_aff(bases, v & 0x7fffffffu);
-    if (v & 0x80000000u) p.y = -p.y;
-    acc = xyzz_madd_aff(acc, p);
+    if (seg_start == gs && e_end == ge) {
+      store_xyzz(bsum, g, acc);
+    } else if (seg_start != gs) {  // first segment, bucket started earlier (it may also go on later)
+      if (join_in_block(gs, ge, K)) shead[threadIdx.x] = acc;
+      else store_xyzz(pfirst, t, acc);
+    } else if (join_in_block(gs, ge, K)) {  // this thread owns a two-piece in-block bucket
+      owner = true;
+    } else {
+      store_xyzz(first ? pfirst : plast, t, acc);
+      multi[atomicAdd(nmulti, 1u)] = g;
+    }
   }
-  if (seg_start == gs && e_end == ge) store_xyzz(bsum, g, acc);
-  else if (first) store_xyzz(pfirst, t, acc);
-  else store_xyzz(plast, t, acc);
+  __syncthreads();
+  if (owner) store_xyzz(bsum, g, xyzz_add(acc, shead[threadIdx.x + 1]));
 }
 
-// Per global bucket: empty -> identity; crossing thread boundaries -> join the pieces.  A bucket
-// spanning more than kFixSerial threads (skewed digits: all-equal scalars, a short top window) is
-// queued for k_fixup_heavy instead of being walked serially.
+// Queued crossing buckets (see k_accumulate): pieces pfirst/plast joined serially when the bucket
+// spans at most kFixSerial + 1 threads; longer ones (skewed digits: all-equal scalars, a short top
+// window) go on to k_fixup_heavy instead of being walked serially.
 static constexpr uint32_t kFixSerial = 8;
-__global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ gst, uint32_t nbt, uint32_t K,
-                                                  const G1Xyzz* __restrict__ pfirst, const G1Xyzz* __restrict__ plast,
-                                                  G1Xyzz* __restrict__ bsum, uint32_t* __restrict__ heavy,
-                                                  uint32_t* __restrict__ nheavy) {
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= nbt) return;
-  uint32_t s = gst[g], e = gst[g + 1];
-  if (s == e) {
-    store_xyzz(bsum, g, G1Xyzz::identity());
-    return;
+__device__ __forceinline__ G1Xyzz fixup_head(const G1Xyzz* __restrict__ pfirst, const G1Xyzz* __restrict__ plast,
+                                             uint32_t s, uint32_t t0, uint32_t K) {
+  return (s == t0 * K) ? load_xyzz(pfirst, t0) : load_xyzz(plast, t0);
+}
+
+// grid-stride over the queue
+__global__ void __launch_bounds__(kBlock) k_fixup_multi(const uint32_t* __restrict__ gst, uint32_t K,
+                                                        const G1Xyzz* __restrict__ pfirst,
+                                                        const G1Xyzz* __restrict__ plast,
+                                                        const uint32_t* __restrict__ multi,
+                                                        const uint32_t* __restrict__ nmulti, G1Xyzz* __restrict__ bsum,
+                                                        uint32_t* __restrict__ heavy, uint32_t* __restrict__ nheavy) {
+  const uint32_t nm = *nmulti;
+  for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < nm; h += gridDim.x * blockDim.x) {
+    const uint32_t g = multi[h];
+    const uint32_t s = gst[g], e = gst[g + 1];
+    const uint32_t t0 = s / K, t1 = (e - 1) / K;
+    if (t1 - t0 > kFixSerial) {
+      heavy[atomicAdd(nheavy, 1u)] = g;
+      continue;
+    }
+    G1Xyzz acc = fixup_head(pfirst, plast, s, t0, K);
+    for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, load_xyzz(pfirst, t));
+    store_xyzz(bsum, g, acc);
   }
-  uint32_t t0 = s / K, t1 = (e - 1) / K;
-  if (t0 == t1) return;
-  if (t1 - t0 > kFixSerial) {
-    heavy[atomicAdd(nheavy, 1u)] = g;
-    return;
-  }
-  G1Xyzz acc = (s == t0 * K) ? load_xyzz(pfirst, t0) : load_xyzz(plast, t0);
-  for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, load_xyzz(pfirst, t));
-  store_xyzz(bsum, g, acc);
 }
 
 // Heavy buckets: one block per queued bucket (grid-stride over the queue), strided partial sums of
@@ -454,8 +579,7 @@ __global__ void __launch_bounds__(kBlock) k_fixup_heavy(const uint32_t* __restri
       __syncthreads();
     }
     if (tid == 0) {
-      G1Xyzz head = (s == t0 * K) ? load_xyzz(pfirst, t0) : load_xyzz(plast, t0);
-      store_xyzz(bsum, g, xyzz_add(head, sh[0]));
+      store_xyzz(bsum, g, xyzz_add(fixup_head(pfirst, plast, s, t0, K), sh[0]));
     }
     __syncthreads();
   }
@@ -463,17 +587,20 @@ __global__ void __launch_bounds__(kBlock) k_fixup_heavy(const uint32_t* __restri
 
 // One bucket-reduction level over `groups` groups of N elements, segments of L buckets:
 //   acc[g][j] = sum_{i in seg j} (i - jL + base) X[g][i],  tot[g][j] = sum_{i in seg j} X[g][i]
-__global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, uint32_t N, uint32_t J, uint32_t L, uint32_t groups, int base,
-                       G1Xyzz* __restrict__ acc_out, G1Xyzz* __restrict__ tot_out) {
+// Empty buckets (gst[b] == gst[b + 1]) are never written by the accumulate pass and read as identity.
+__global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, const uint32_t* __restrict__ gst,
+                                                 uint32_t N, uint32_t J, uint32_t L, uint32_t groups, int base,
+                                                 G1Xyzz* __restrict__ acc_out, G1Xyzz* __restrict__ tot_out) {
   uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= J * groups) return;
   uint32_t g = tid / J, j = tid % J;
   const G1Xyzz* x = X + (size_t)g * N;
+  const uint32_t* gs = gst + (size_t)g * N;
   uint32_t lo = j * L;
   uint32_t hi = min(N, lo + L);
   G1Xyzz run = G1Xyzz::identity(), acc = G1Xyzz::identity();
   for (uint32_t i = hi; i-- > lo;) {
-    run = xyzz_add(run, load_xyzz(x, i));
+    if (gs[i] != gs[i + 1]) run = xyzz_add(run, load_xyzz(x, i));
     if (base || i > lo) acc = xyzz_add(acc, run);
   }
   store_xyzz(acc_out, tid, acc);
@@ -524,17 +651,28 @@ static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b -
 
 MsmPlan msm_plan(size_t n) {
   MsmPlan p;
+  // GLV (k P = k1 P + k2 phi(P), 128-bit halves) halves the buckets, the bucket reduction and the
+  // Horner chain for the same number of bucket entries, but costs the split, a stored phi(P) table
+  // and a slower sort; measured at 2^20 it lost overall (tail work is not what bounds the tail at
+  // one wave per SIMD) and at 2^24 the doubled table slowed the fill (31 -> 36 ms).  Kept behind
+  // SVGPU_GLV / SVGPU_GLV_MAX_LOG (tests run it both ways).
+  int glv_max_log = 0;  // off by default: measured slower at 2^20 (2.38 vs 2.33 ms; the split + phi table cost more than the halved tail)
+  if (const char* e = getenv("SVGPU_GLV_MAX_LOG")) glv_max_log = atoi(e);
+  p.glv = n >= (size_t(1) << 14) && n <= (size_t(1) << glv_max_log);
+  if (const char* e = getenv("SVGPU_GLV")) p.glv = atoi(e) != 0 && n >= 2;
+  p.npts = p.glv ? 2 * n : n;
+  const int nb = p.glv ? 128 : 255;
   int lg = 0;
-  while ((size_t(1) << (lg + 1)) <= n) lg++;
+  while ((size_t(1) << (lg + 1)) <= p.npts) lg++;
   int c = lg - 4;
   if (const char* e = getenv("SVGPU_WINDOW_BITS")) c = atoi(e);
   if (c < 4) c = 4;
   if (c > 16) c = 16;
   p.c = c;
-  p.W = (255 + c - 1) / c;
+  p.W = (nb + c - 1) / c;
   p.B = 1u << (c - 1);
   p.nbt = p.B * p.W;
-  uint64_t entries = (uint64_t)n * p.W;
+  uint64_t entries = (uint64_t)p.npts * p.W;
   uint64_t K = entries / (1u << 18);
   if (K < 4) K = 4;
   if (K > 32) K = 32;
@@ -576,22 +714,29 @@ MsmPlan msm_plan(size_t n) {
     default: break;                                                            \
   }
 
-#define SV_LAUNCH_C(KERNEL, C, GRID, BLOCK, ...)                                \
-  switch (C) {                                                                 \
-    case 4: hipLaunchKernelGGL(KERNEL<4>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
-    case 5: hipLaunchKernelGGL(KERNEL<5>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
-    case 6: hipLaunchKernelGGL(KERNEL<6>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
-    case 7: hipLaunchKernelGGL(KERNEL<7>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
-    case 8: hipLaunchKernelGGL(KERNEL<8>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
-    case 9: hipLaunchKernelGGL(KERNEL<9>, GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
-    case 10: hipLaunchKernelGGL(KERNEL<10>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
-    case 11: hipLaunchKernelGGL(KERNEL<11>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
-    case 12: hipLaunchKernelGGL(KERNEL<12>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
-    case 13: hipLaunchKernelGGL(KERNEL<13>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
-    case 14: hipLaunchKernelGGL(KERNEL<14>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
-    case 15: hipLaunchKernelGGL(KERNEL<15>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
-    case 16: hipLaunchKernelGGL(KERNEL<16>, GRID, BLOCK, 0, st, __VA_ARGS__); break; \
-    default: break;                                                            \
+#define SV_LAUNCH_C1(KERNEL, NB, C, GRID, BLOCK, ...)                                              \
+  switch (C) {                                                                                   \
+    case 4: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<4, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 5: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<5, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 6: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<6, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 7: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<7, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 8: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<8, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 9: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<9, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 10: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<10, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 11: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<11, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 12: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<12, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 13: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<13, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 14: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<14, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 15: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<15, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 16: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<16, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    default: break;                                                                              \
+  }
+// full scalars (NB = 255) or GLV halves (NB = 128)
+#define SV_LAUNCH_C(KERNEL, GLV, C, GRID, BLOCK, ...)              \
+  if (GLV) {                                                       \
+    SV_LAUNCH_C1(KERNEL, 128, C, GRID, BLOCK, __VA_ARGS__)         \
+  } else {                                                         \
+    SV_LAUNCH_C1(KERNEL, 255, C, GRID, BLOCK, __VA_ARGS__)         \
   }
 
 // Host Horner over (window, group) terms: total = sum_w 2^(c w) [A_lo + A_hi + sum_k 2^(2+k) U_k].
@@ -630,17 +775,19 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
   Workspace* ws = lease.get();
   hipStream_t st = ws->stream;
   const MsmPlan p = msm_plan(n);
-  const uint64_t entries = (uint64_t)n * p.W;
+  const uint64_t entries = (uint64_t)p.npts * p.W;
 
   // ---- workspace layout
   const int LOGB = p.c - 1;
-  const uint32_t CB = LOGB < 6 ? (uint32_t)LOGB : 6u, FB = (uint32_t)LOGB - CB, NBIN = 1u << CB;
+  const uint32_t CB = (uint32_t)coarse_bits(p.c, p.glv ? 128 : 255), FB = (uint32_t)LOGB - CB, NBIN = 1u << CB;
   const uint32_t nwb = p.W * NBIN;
-  const uint32_t nblk = cdiv(n, sort_chunk(p.c));
+  const uint32_t nblk = cdiv(p.npts, sort_chunk(p.c, p.glv ? 128 : 255));
   size_t bytes = 0;
   auto add = [&](size_t b) { bytes += Workspace::aligned(b); };
   bool conv = (form == SV_CANONICAL);
   if (conv) add(n * sizeof(G1Aff));
+  if (p.glv) add(2 * n * sizeof(uint4));      // GLV scalar halves
+  if (p.glv) add(n * sizeof(G1Aff));          // phi(P)
   add(256);                                   // err flag + heavy-queue counter
   add((size_t)nwb * nblk * 4);                // bcnt
   add((size_t)nwb * 4);                       // btot
@@ -652,6 +799,7 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
   add((size_t)p.T * sizeof(G1Xyzz) * 2);      // pfirst, plast
   add((size_t)p.nbt * sizeof(G1Xyzz));        // bsum
   add((size_t)p.nbt * 4);                     // heavy-bucket queue
+  add((size_t)p.nbt * 4);                     // multi-thread-bucket queue
   const size_t nfinal = (size_t)p.W * p.NG;
   add((size_t)p.J * p.W * sizeof(G1Xyzz) * 2);  // acc_j, T_j
   add(nfinal * sizeof(G1Xyzz));                 // group sums
@@ -662,6 +810,8 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
   const Fr* scalars = reinterpret_cast<const Fr*>(d_scalars);
   const int mont_in = form == SV_MONTGOMERY ? 1 : 0;
   G1Aff* bases_m = conv ? ws->carve<G1Aff>(n) : nullptr;
+  uint4* hs = p.glv ? ws->carve<uint4>(2 * n) : nullptr;
+  G1Aff* phi = p.glv ? ws->carve<G1Aff>(n) : nullptr;
   uint32_t* err = ws->carve<uint32_t>(64);
   uint32_t* bcnt = ws->carve<uint32_t>((size_t)nwb * nblk);
   uint32_t* btot = ws->carve<uint32_t>(nwb);
@@ -674,7 +824,9 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
   G1Xyzz* plast = ws->carve<G1Xyzz>(p.T);
   G1Xyzz* bsum = ws->carve<G1Xyzz>(p.nbt);
   uint32_t* heavy = ws->carve<uint32_t>(p.nbt);
+  uint32_t* multi = ws->carve<uint32_t>(p.nbt);
   uint32_t* nheavy = err + 1;  // zeroed with the error flag
+  uint32_t* nmulti = err + 2;
   G1Xyzz* racc = ws->carve<G1Xyzz>((size_t)p.J * p.W);
   G1Xyzz* rtot = ws->carve<G1Xyzz>((size_t)p.J * p.W);
   G1Xyzz* ping = ws->carve<G1Xyzz>(nfinal);
@@ -687,28 +839,42 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
                        bases, bases_m, (uint32_t)n, err);
     bases = bases_m;
   }
-  SV_LAUNCH_C(k_bin_hist, p.c, dim3(nblk), dim3(kBlock), scalars, (uint32_t)n, mont_in, nblk, bcnt, err);
+  const void* dsrc = scalars;  // what the sort passes take digits from
+  if (p.glv) {
+    hipLaunchKernelGGL(k_glv_prep, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, st, bases, scalars, (uint32_t)n, mont_in,
+                       hs, phi, err);
+    dsrc = hs;
+  }
+  const uint32_t npts = (uint32_t)p.npts;
+  SV_LAUNCH_C(k_bin_hist, p.glv, p.c, dim3(nblk), dim3(kBlock), dsrc, npts, mont_in, nblk, bcnt, err);
   SV_HIP(hipGetLastError());
   SV_HIP(hipEventRecord(ev[1], st));
   hipLaunchKernelGGL(k_bin_scan_chunks, dim3(nwb), dim3(kBlock), 0, st, bcnt, nblk, btot);
   hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, btot, nwb, bstart);
-  SV_LAUNCH_C(k_bin_scatter, p.c, dim3(nblk), dim3(kBlock), scalars, (uint32_t)n, mont_in, nblk, bcnt, bstart,
+  SV_LAUNCH_C(k_bin_scatter, p.glv, p.c, dim3(nblk), dim3(kBlock), dsrc, npts, mont_in, nblk, bcnt, bstart,
               tmp);
-  hipLaunchKernelGGL(k_fine_sort, dim3(nwb), dim3(1024), 0, st, tmp, bstart, FB, p.K, gst, tstart, ent);
+  static thread_local int fine_attr_dev = -1;  // the > 64 KiB dynamic-LDS opt-in, once per thread/device
+  if (fine_attr_dev != device) {
+    SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFineLds));
+    fine_attr_dev = device;
+  }
+  hipLaunchKernelGGL(k_fine_sort, dim3(nwb), dim3(1024), kFineLds, st, tmp, bstart, FB, p.K, gst, tstart, ent);
   SV_HIP(hipMemcpyAsync(gst + p.nbt, bstart + nwb, 4, hipMemcpyDeviceToDevice, st));
   SV_HIP(hipGetLastError());
   SV_HIP(hipEventRecord(ev[2], st));
   hipLaunchKernelGGL(k_accumulate, dim3(cdiv(p.T, kBlock)), dim3(kBlock), 0, st, bases, ent, gst,
-                     tstart, p.nbt, p.K, p.T, bsum, pfirst, plast);
+                     tstart, p.nbt, p.K, p.T, bsum, pfirst, plast, multi, nmulti, phi,
+                     p.glv ? (uint32_t)n : ~0u);
   SV_HIP(hipGetLastError());
   SV_HIP(hipEventRecord(ev[3], st));
-  hipLaunchKernelGGL(k_fixup, dim3(cdiv(p.nbt, kBlock)), dim3(kBlock), 0, st, gst, p.nbt, p.K, pfirst,
-                     plast, bsum, heavy, nheavy);
+  hipLaunchKernelGGL(k_fixup_multi, dim3(std::min<uint32_t>(cdiv(p.nbt, kBlock), 1024)), dim3(kBlock), 0, st,
+                     gst, p.K, pfirst, plast, multi, nmulti, bsum, heavy, nheavy);
   hipLaunchKernelGGL(k_fixup_heavy, dim3(256), dim3(kBlock), 0, st, gst, p.K, pfirst, plast, heavy, nheavy,
                      bsum);
   SV_HIP(hipEventRecord(ev[4], st));
   // bucket reduction: running sums over segments of 2^logL buckets, then the subset sums
-  hipLaunchKernelGGL(k_wsum, dim3(cdiv((uint64_t)p.J * p.W, kBlock)), dim3(kBlock), 0, st, bsum, p.B, p.J,
+  hipLaunchKernelGGL(k_wsum, dim3(cdiv((uint64_t)p.J * p.W, kBlock)), dim3(kBlock), 0, st, bsum, gst, p.B, p.J,
                      1u << p.logL, p.W, 1, racc, rtot);
   hipLaunchKernelGGL(k_group_sum, dim3(p.NG * p.W), dim3(kGroupBlock), 0, st, racc, rtot, p.J, p.logJ, ping);
   SV_HIP(hipGetLastError());

@@ -21,6 +21,8 @@ struct MsmPlan {
   uint32_t J;       // running-sum segments per window (B >> logL)
   uint32_t logJ;    // log2(J)
   uint32_t NG;      // subset-sum groups per window: 2 + logJ
+  bool glv;         // GLV split: 2n virtual points (P, phi(P)) with 128-bit scalar halves
+  size_t npts;      // virtual points: n, or 2n with GLV
 };
 
 MsmPlan msm_plan(size_t n);

@@ -171,12 +171,14 @@ def test_window_bits_override(gpu, oracle_cpp, bits, monkeypatch):
     assert svgpu.msm_arrays(B, S) == _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
 
 
-def test_edge_scalars(gpu, oracle_cpp):
-    """Scalars at window and GLV-decomposition edges (k = lambda gives k1 = 0, k2 = 1 in the
-    batched path's split; multiples and neighbours of lambda, of r, of 2^127 / 2^128) against the
-    reference Pippenger restatement."""
+@pytest.mark.parametrize("glv", ["0", "1"])
+def test_edge_scalars(gpu, oracle_cpp, glv, monkeypatch):
+    """Scalars at window and GLV-decomposition edges (k = lambda gives k1 = 0, k2 = 1; multiples and
+    neighbours of lambda, of r, of 2^127 / 2^128) against the reference Pippenger restatement, with
+    the single-MSM pipeline's GLV split forced off and on (SVGPU_GLV)."""
     import random
     import svgpu
+    monkeypatch.setenv("SVGPU_GLV", glv)
     from svgpu import encoding as enc
     lam = 0xB3C4D79D41A917585BFC41088D8DAAA78B17EA66B99C90DD
     r = b.R
@@ -194,3 +196,23 @@ def test_edge_scalars(gpu, oracle_cpp):
     for k in ks[:19]:
         Sk = enc.scalars_array([k])
         assert svgpu.msm_arrays(B[:1], Sk) == _to_pt(oracle_cpp.msm_pippenger(B[:1], Sk, 0)), hex(k)
+
+
+@pytest.mark.parametrize("glv", ["0", "1"])
+@pytest.mark.parametrize("n", [2, 3, 65, 4097, 20000, 65537])
+def test_glv_split_on_off(gpu, oracle_cpp, n, glv, monkeypatch):
+    """The single-MSM pipeline with and without the GLV split (2n virtual points, 128-bit halves,
+    phi(P) table) gives the reference Pippenger's point, both input forms."""
+    import svgpu
+    from svgpu import encoding as enc
+    monkeypatch.setenv("SVGPU_GLV", glv)
+    B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=31 * n)
+    S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=31 * n)
+    exp = _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
+    assert svgpu.msm_arrays(B, S, svgpu.SV_CANONICAL) == exp
+    if n <= 4097:
+        pts = [enc.g1_from_limbs(r) for r in B]
+        sc = [enc.limbs_to_int(r) for r in S]
+        Bm = enc.bases_array(pts, svgpu.SV_MONTGOMERY)
+        Sm = enc.scalars_array(sc, svgpu.SV_MONTGOMERY)
+        assert svgpu.msm_arrays(Bm, Sm, svgpu.SV_MONTGOMERY) == exp

@@ -1,0 +1,34 @@
+"""Time the 2^k MSM under several tuning-env settings (one process; every result checked equal).
+Usage: python tools/msm_sweep_env.py LOG_N 'SVGPU_GLV=1,SVGPU_ACC_K=64' 'SVGPU_GLV=0' ..."""
+import os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "snark-verifier-axiom_amd")); sys.path.insert(0, ROOT)
+import torch, svgpu
+from svgpu import device as dv
+from oracle import bn254 as ob
+svgpu.init()
+dev = torch.device("cuda:0")
+log_n = int(sys.argv[1])
+n = 1 << log_n
+B = dv.gen_bases(dv.empty_bases(n, dev), ob.SEED_BASES, 0)
+S = dv.gen_scalars(dv.empty_scalars(n, dev), ob.SEED_SCALARS, 0)
+torch.cuda.synchronize()
+KEYS = ("SVGPU_GLV", "SVGPU_ACC_K", "SVGPU_RED_LOG", "SVGPU_WINDOW_BITS", "SVGPU_GLV_MAX_LOG")
+ref = None
+for rnd in range(2):
+    for spec in sys.argv[2:]:
+        for k in KEYS:
+            os.environ.pop(k, None)
+        for kv in filter(None, spec.split(",")):
+            k, v = kv.split("=")
+            os.environ[k] = v
+        r = dv.msm(B, S)
+        ref = r if ref is None else ref
+        ts = []
+        for _ in range(7):
+            t0 = time.perf_counter(); r2 = dv.msm(B, S); ts.append(time.perf_counter() - t0)
+        st = dv.last_msm_stats()
+        ts.sort()
+        print(f"2^{log_n} [{spec}] c={st['window_bits']} W={st['num_windows']}: med {1e3*ts[3]:.3f} min {1e3*ts[0]:.3f} ms "
+              f"ok={r == ref == r2} digits={st['digits_ms']:.3f} sort={st['sort_ms']:.3f} acc={st['accumulate_ms']:.3f} "
+              f"fix={st['fixup_ms']:.3f} red={st['reduce_ms']:.3f} host={st['host_ms']:.3f}", flush=True)

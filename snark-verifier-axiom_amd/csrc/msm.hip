@@ -371,10 +371,14 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const void* __restrict__
 // from tmp ONCE into registers and sorted into an LDS copy of the region, which is then written to
 // ent[] with consecutive lanes on consecutive addresses: the direct scatter of 4-byte entries to
 // global memory cost ~5x its bytes in partial-line write traffic (PMC WRITE_SIZE, r01).  Larger
-// regions take the two-read global-scatter path.
+// regions are processed in LDS chunks of the same size (below); the two cases are separate
+// instantiations (BIG), each block leaving at once unless its region is of its kind, so the staged
+// one keeps to <= 64 VGPRs (two 1024-thread blocks per CU).
 static constexpr uint32_t kFineR = 18;                 // entries per thread held in registers
 static constexpr uint32_t kFineCap = 1024 * kFineR;    // region entries staged in LDS
+static constexpr uint32_t kChunkR = 12, kChunk = 1024 * kChunkR;  // large regions: LDS chunk
 static constexpr size_t kFineLds = (512 + 1024 + (size_t)kFineCap) * 4;  // 78 KiB: 2 blocks per CU
+template <bool BIG>
 __global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__ tmp,
                                                     const uint32_t* __restrict__ bstart, uint32_t FB, uint32_t K,
                                                     uint32_t* __restrict__ gst, uint32_t* __restrict__ tstart,
@@ -385,11 +389,12 @@ __global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__
   uint32_t* out = fine_lds + 1536;   // [kFineCap] the sorted region
   const uint32_t wb = blockIdx.x, tid = threadIdx.x, NF = 1u << FB;
   const uint32_t s0 = bstart[wb], s1 = bstart[wb + 1], len = s1 - s0;
-  const bool staged = len <= kFineCap;  // block-uniform
+  if ((len > kFineCap) != BIG) return;  // block-uniform
+  constexpr bool staged = !BIG;
   for (uint32_t f = tid; f < NF; f += 1024) fc[f] = 0;
   __syncthreads();
   uint64_t x[kFineR];
-  if (staged) {
+  if constexpr (staged) {
 #pragma unroll
     for (uint32_t r = 0; r < kFineR; r++) {
       const uint32_t i = tid + r * 1024;
@@ -429,7 +434,7 @@ __global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__
     for (uint32_t t = (st + K - 1) / K; t * K < en; t++) tstart[t] = g;
   }
   __syncthreads();
-  if (staged) {
+  if constexpr (staged) {
 #pragma unroll
     for (uint32_t r = 0; r < kFineR; r++)
       if (tid + r * 1024 < len) out[atomicAdd(&fc[(uint32_t)(x[r] >> 32)], 1u)] = (uint32_t)x[r];
@@ -437,17 +442,63 @@ __global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__
     for (uint32_t i = tid; i < len; i += 1024) ent[s0 + i] = out[i];
     return;
   }
-  uint32_t e = s0 + tid;
-  for (; e + 3 * 1024 < s1; e += 4 * 1024) {
-    uint64_t y[4];
+  // Large region: chunks of kChunk entries (12 per thread: the instantiation stays <= 64 VGPRs), each counting-sorted in LDS (chunk-local counts lc,
+  // starts ls) and written as one contiguous run per fine bucket at that bucket's global cursor fc.
+  uint32_t* lc = part;  // chunk counts reuse the scan buffer's first 512 words ...
+  uint32_t* ls = part + 512;  // ... and chunk-local starts its second half
+  for (uint32_t c0 = s0; c0 < s1; c0 += kChunk) {
+    const uint32_t clen = min(kChunk, s1 - c0);
+    if (tid < NF) lc[tid] = 0;
+    __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 4; j++) y[j] = tmp[e + j * 1024];
+    for (uint32_t r = 0; r < kChunkR; r++) {
+      const uint32_t i = tid + r * 1024;
+      x[r] = i < clen ? tmp[c0 + i] : 0;
+      if (i < clen) atomicAdd(&lc[(uint32_t)(x[r] >> 32)], 1u);
+    }
+    __syncthreads();
+    // exclusive scan of lc[0 .. NF) by one wave per 64 buckets + a serial pass over the 8 totals
+    if (tid < NF) {
+      uint32_t v2 = lc[tid], incl = v2;
 #pragma unroll
-    for (int j = 0; j < 4; j++) ent[atomicAdd(&fc[(uint32_t)(y[j] >> 32)], 1u)] = (uint32_t)y[j];
-  }
-  for (; e < s1; e += 1024) {
-    const uint64_t y = tmp[e];
-    ent[atomicAdd(&fc[(uint32_t)(y >> 32)], 1u)] = (uint32_t)y;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(incl, o);
+        if ((tid & 63) >= (uint32_t)o) incl += u;
+      }
+      ls[tid] = incl - v2;  // exclusive within the wave
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t run = 0;
+      for (uint32_t w = 0; w < NF; w += 64) {
+        const uint32_t last = min(NF, w + 64) - 1;
+        const uint32_t tot = ls[last] + lc[last];
+        out[kFineCap - 8 + (w >> 6)] = run;  // per-wave offsets parked at the end of out[]
+        run += tot;
+      }
+    }
+    __syncthreads();
+    uint32_t base_f = 0;
+    if (tid < NF) base_f = ls[tid] + out[kFineCap - 8 + (tid >> 6)];
+    __syncthreads();
+    if (tid < NF) {
+      ls[tid] = base_f;
+      lc[tid] = base_f;  // lc becomes the chunk-local cursor
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < kChunkR; r++)
+      if (tid + r * 1024 < clen) out[atomicAdd(&lc[(uint32_t)(x[r] >> 32)], 1u)] = (uint32_t)x[r];
+    __syncthreads();
+    // one wave per fine bucket run: out[ls[f] .. lc[f]) -> ent[fc[f] ..), consecutive lanes on
+    // consecutive addresses
+    for (uint32_t f = tid >> 6; f < NF; f += 16) {
+      const uint32_t st = ls[f], cnt = lc[f] - st, dst = fc[f];
+      for (uint32_t j = tid & 63; j < cnt; j += 64) ent[dst + j] = out[st + j];
+    }
+    __syncthreads();
+    if (tid < NF) fc[tid] += lc[tid] - ls[tid];
+    __syncthreads();
   }
 }
 
@@ -676,10 +727,12 @@ MsmPlan msm_plan(size_t n) {
   uint64_t K = entries / (1u << 18);
   if (K < 4) K = 4;
   if (K > 32) K = 32;
-  // large n: buckets average entries / nbt >> 32 entries; keep a bucket within ~2-3 threads so the
-  // fixup stays a short serial join (a 2^24 MSM at c = 16 has 512 entries per bucket)
-  const uint64_t half_bucket = entries / p.nbt / 2;
-  if (K < half_bucket) K = half_bucket < 512 ? half_bucket : 512;
+  // large n: buckets average entries / nbt > 32 entries; a chunk of about one average bucket keeps
+  // most crossing buckets at two pieces (joined inside k_accumulate), capped at 256 entries so the
+  // grid still has many rounds of waves (swept, tools/gpu_sweep_big.sh: 2^21 K = 64 4.47 -> 4.41 ms;
+  // 2^24 K = 256 32.0 ms, 512 32.4, 1024 33.4)
+  const uint64_t avg_bucket = entries / p.nbt;
+  if (K < avg_bucket) K = avg_bucket < 256 ? avg_bucket : 256;
   if (const char* e = getenv("SVGPU_ACC_K")) K = (uint64_t)atoi(e);
   if (K < 1) K = 1;
   p.K = (uint32_t)K;
@@ -855,11 +908,14 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
               tmp);
   static thread_local int fine_attr_dev = -1;  // the > 64 KiB dynamic-LDS opt-in, once per thread/device
   if (fine_attr_dev != device) {
-    SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort),
+    SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort<false>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFineLds));
+    SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort<true>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFineLds));
     fine_attr_dev = device;
   }
-  hipLaunchKernelGGL(k_fine_sort, dim3(nwb), dim3(1024), kFineLds, st, tmp, bstart, FB, p.K, gst, tstart, ent);
+  hipLaunchKernelGGL(k_fine_sort<false>, dim3(nwb), dim3(1024), kFineLds, st, tmp, bstart, FB, p.K, gst, tstart, ent);
+  hipLaunchKernelGGL(k_fine_sort<true>, dim3(nwb), dim3(1024), kFineLds, st, tmp, bstart, FB, p.K, gst, tstart, ent);
   SV_HIP(hipMemcpyAsync(gst + p.nbt, bstart + nwb, 4, hipMemcpyDeviceToDevice, st));
   SV_HIP(hipGetLastError());
   SV_HIP(hipEventRecord(ev[2], st));

@@ -181,7 +181,8 @@ int sv_gen_bases_device(sv_g1_affine* d_bases, size_t n, uint64_t seed, uint64_t
                         int device, void* stream) SV_NOEXCEPT;
 
 /* ---- instrumentation ----------------------------------------------------------------
- * Per-kernel timings (HIP events on the call's stream) of the last MSM on this thread.   */
+ * Per-kernel timings (HIP events on the call's stream) of the last MSM on this thread; the digits
+ * and fixup splits are filled only with SVGPU_MSM_STATS=1 (folded into sort / reduce otherwise). */
 typedef struct {
   float total_ms, digits_ms, sort_ms, accumulate_ms, fixup_ms, reduce_ms, host_ms;
   uint32_t window_bits, num_windows, accumulate_launch_units;

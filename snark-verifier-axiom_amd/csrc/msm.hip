@@ -44,6 +44,9 @@
 namespace sv {
 
 static constexpr int kBlock = 256;
+#ifndef SV_ACC_PREFETCH
+#define SV_ACC_PREFETCH 1  // next entry index loaded a step ahead (0: none, 2: next point too -- 138 VGPRs, no gain)
+#endif
 
 __device__ __forceinline__ G1Aff load_aff(const G1Aff* __restrict__ a, uint32_t i) {
   const uint4* p = reinterpret_cast<const uint4*>(a + i);
@@ -537,6 +540,16 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
     ge = gst[g + 1];
     uint32_t seg_start = s0;
     bool first = true;
+#if SV_ACC_PREFETCH >= 1
+    uint32_t vnext = ent[s0];
+#endif
+#if SV_ACC_PREFETCH >= 2
+    G1Aff pnext;
+    {
+      const uint32_t idx = vnext & 0x7fffffffu;
+      pnext = load_aff(idx >= nsplit ? phi + (idx - nsplit) : bases + idx, 0);
+    }
+#endif
     for (uint32_t e = s0; e < e_end; e++) {
       if (e >= ge) {  // segment [seg_start, ge) of bucket g ends inside this chunk
         if (seg_start == gs) {
@@ -554,9 +567,23 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
         seg_start = e;
         acc = G1Xyzz::identity();
       }
+#if SV_ACC_PREFETCH == 0
       const uint32_t v = ent[e], idx = v & 0x7fffffffu;
       // virtual point idx: P_idx, or phi(P_(idx - n)) for the GLV halves (nsplit = n; ~0u without GLV)
       G1Aff p = load_aff(idx >= nsplit ? phi + (idx - nsplit) : bases + idx, 0);
+#elif SV_ACC_PREFETCH == 1
+      const uint32_t v = vnext, idx = v & 0x7fffffffu;
+      if (e + 1 < e_end) vnext = ent[e + 1];
+      G1Aff p = load_aff(idx >= nsplit ? phi + (idx - nsplit) : bases + idx, 0);
+#else
+      const uint32_t v = vnext;
+      G1Aff p = pnext;
+      if (e + 1 < e_end) {  // next entry's point in flight during this addition
+        vnext = ent[e + 1];
+        const uint32_t idx = vnext & 0x7fffffffu;
+        pnext = load_aff(idx >= nsplit ? phi + (idx - nsplit) : bases + idx, 0);
+      }
+#endif
       if (v & 0x80000000u) p.y = -p.y;
       acc = xyzz_madd_aff(acc, p);
     }

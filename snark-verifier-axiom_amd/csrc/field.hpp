@@ -246,6 +246,24 @@ __device__ __forceinline__ void mac_carry4(uint64_t& acc, uint32_t& ovf, const u
       : "v"(x[0]), "v"(y[0]), "v"(x[1]), "v"(y[1]), "v"(x[2]), "v"(y[2]), "v"(x[3]), "v"(y[3])
       : "vcc");
 }
+// Column-opening forms: the first product's carry initialises ovf (v_cndmask from VCC) instead of
+// a v_mov of 0 before the column -- one instruction less per column (16 per multiplication).
+#define SV_MAC_FIRST(A, B) "v_mad_u64_u32 %0, vcc, " A ", " B ", %0\n\tv_cndmask_b32_e64 %1, 0, 1, vcc\n\t"
+__device__ __forceinline__ void mac_first(uint64_t& acc, uint32_t& ovf, uint32_t a, uint32_t b) {
+  asm(SV_MAC_FIRST("%2", "%3") : "+v"(acc), "=v"(ovf) : "v"(a), "v"(b) : "vcc");
+}
+__device__ __forceinline__ void mac_first2(uint64_t& acc, uint32_t& ovf, uint32_t a0, uint32_t b0, uint32_t a1,
+                                           uint32_t b1) {
+  asm(SV_MAC_FIRST("%2", "%3") SV_MAC_STEP("%4", "%5")
+      : "+v"(acc), "=&v"(ovf) : "v"(a0), "v"(b0), "v"(a1), "v"(b1) : "vcc");
+}
+__device__ __forceinline__ void mac_first4(uint64_t& acc, uint32_t& ovf, const uint32_t* x, const uint32_t* y) {
+  asm(SV_MAC_FIRST("%2", "%3") SV_MAC_STEP("%4", "%5") SV_MAC_STEP("%6", "%7") SV_MAC_STEP("%8", "%9")
+      : "+v"(acc), "=&v"(ovf)
+      : "v"(x[0]), "v"(y[0]), "v"(x[1]), "v"(y[1]), "v"(x[2]), "v"(y[2]), "v"(x[3]), "v"(y[3])
+      : "vcc");
+}
+#undef SV_MAC_FIRST
 #undef SV_MAC_STEP
 
 // Montgomery multiplication by finely integrated product scanning: column k accumulates
@@ -278,7 +296,23 @@ SV_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
         c++;
       }
     }
+    // the column's first asm block opens ovf (mac_first*); a column with no products before the
+    // m_k step (k = 0) opens it there; the empty last column (k = 15) sets it to 0
     int q = 0;
+    bool open = false;
+    if (c >= 4) {
+      mac_first4(acc, ovf, xs, ys);
+      q = 4;
+      open = true;
+    } else if (c >= 2) {
+      mac_first2(acc, ovf, xs[0], ys[0], xs[1], ys[1]);
+      q = 2;
+      open = true;
+    } else if (c == 1) {
+      mac_first(acc, ovf, xs[0], ys[0]);
+      q = 1;
+      open = true;
+    }
 #pragma unroll
     for (; q + 3 < c; q += 4) mac_carry4(acc, ovf, xs + q, ys + q);
 #pragma unroll
@@ -287,12 +321,13 @@ SV_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
     for (; q < c; q++) mac_carry(acc, ovf, xs[q], ys[q]);
     if (k < 8) {
       m[k] = (uint32_t)acc * M::NP0;
-      mac_carry(acc, ovf, m[k], M::p(0));
+      if (open) mac_carry(acc, ovf, m[k], M::p(0));
+      else mac_first(acc, ovf, m[k], M::p(0));
     } else {
       t[k - 8] = (uint32_t)acc;
+      if (!open) ovf = 0;
     }
     acc = (acc >> 32) | ((uint64_t)ovf << 32);
-    ovf = 0;
   }
   const uint32_t top = (uint32_t)acc;
   Fe<M> d;

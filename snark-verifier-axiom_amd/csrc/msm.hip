@@ -201,6 +201,7 @@ __host__ __device__ constexpr uint32_t sort_chunk(int c, int nb = 255) { return 
 // coarse bits: 2^CB bins per window, so that W * 2^CB ~ 1024 fine-sort regions of ~16K entries at
 // 2^20 (LDS-staged in k_fine_sort) -- 64 bins for the 16 full-width windows, 128 for the 8 GLV ones
 __host__ __device__ constexpr int coarse_bits(int c, int nb) { return c - 1 < (nb == 128 ? 7 : 6) ? c - 1 : (nb == 128 ? 7 : 6); }
+__host__ __device__ constexpr int ceil_log2(int x) { return x <= 1 ? 0 : 1 + ceil_log2((x + 1) / 2); }
 
 // exclusive scan of x[0 .. N) in LDS by a 256-thread block (N <= 4096); returns the total
 template <int N>
@@ -318,13 +319,14 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const void* __restrict__
                                                         uint64_t* __restrict__ tmp) {
   constexpr int W = num_windows<C, NB>(), LOGB = C - 1;
   constexpr int CB = coarse_bits(C, NB), FB = LOGB - CB, NBIN = 1 << CB, NK = W * NBIN;
+  // staged entry: local point (9 bits) | sign << 9 | fine << 10 | (window, bin) key << (10 + FB)
+  static_assert(10 + FB + ceil_log2(NK) <= 32, "staged entry overflows 32 bits");
   constexpr uint32_t FMASK = (1u << FB) - 1;
   constexpr uint32_t CH = sort_chunk(C, NB), PT = CH / kBlock;
   __shared__ uint32_t off[NK];   // local group offsets
   __shared__ uint32_t cur[NK];   // cursors
   __shared__ uint32_t part[kBlock];
-  __shared__ uint32_t stage[CH * W];  // local point (9 bits) | sign << 9 | fine << 10
-  __shared__ uint16_t key[CH * W];
+  __shared__ uint32_t stage[CH * W];  // see the layout above (no separate key array: 3 blocks per CU)
   const uint32_t blk = blockIdx.x, lo = blk * CH, hi = min(n, lo + CH);
   for (int k = threadIdx.x; k < NK; k += kBlock) off[k] = 0;
   __syncthreads();
@@ -353,8 +355,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const void* __restrict__
           const uint32_t b = mag - 1;
           const uint32_t k = w * NBIN + (b >> FB);
           const uint32_t pos = atomicAdd(&cur[k], 1u);
-          stage[pos] = li | ((neg ^ sg[j]) << 9) | ((b & FMASK) << 10);
-          key[pos] = (uint16_t)k;
+          stage[pos] = li | ((neg ^ sg[j]) << 9) | ((b & FMASK) << 10) | (k << (10 + FB));
         }
       });
     }
@@ -365,7 +366,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const void* __restrict__
   __syncthreads();
   for (uint32_t x = threadIdx.x; x < total; x += kBlock) {
     const uint32_t e = stage[x];
-    tmp[cur[key[x]] + x] = ((uint64_t)(e >> 10) << 32) | (lo + (e & 511u)) | (((e >> 9) & 1u) << 31);
+    tmp[cur[e >> (10 + FB)] + x] = ((uint64_t)((e >> 10) & FMASK) << 32) | (lo + (e & 511u)) | (((e >> 9) & 1u) << 31);
   }
 }
 
@@ -859,6 +860,8 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
 
   // ---- workspace layout
   const int LOGB = p.c - 1;
+  // (128 coarse bins for 2^21 full-width points, LDS-staged regions, measured no faster: the scatter
+  // runs and the per-block count table grow as much as the fine sort saves)
   const uint32_t CB = (uint32_t)coarse_bits(p.c, p.glv ? 128 : 255), FB = (uint32_t)LOGB - CB, NBIN = 1u << CB;
   const uint32_t nwb = p.W * NBIN;
   const uint32_t nblk = cdiv(p.npts, sort_chunk(p.c, p.glv ? 128 : 255));

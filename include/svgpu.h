@@ -119,6 +119,29 @@ int sv_bn254_g1_msm_batch_device(const sv_g1_affine* d_bases, const sv_fe* d_sca
                                  int form, int device, void* stream,
                                  sv_g1_affine* d_out) SV_NOEXCEPT;
 
+/* ---- device-resident fixed bases for batched MSMs ------------
+ * A native verifier's constant bases -- the generator and the circuit's preprocessed
+ * commitments, loaded once per verifier (Protocol::loaded, plonk/protocol.rs:106-131; used by
+ * the per-proof Msm::evaluate of bdfg21.rs:75-78 / gwc19.rs:76-79) -- are uploaded ONCE as a
+ * base table (stored in Montgomery form on `device`; coordinates must be reduced) and then
+ * referenced by index, so a per-proof batch ships only scalars and u32 indices:
+ *   MSM k = sum_{i in [offsets[k], offsets[k+1])} scalars[i] * table[base_idx[i]].
+ * An index >= the table length is SV_ERR_ARG; an empty MSM is SV_ERR_EMPTY.  Handles are
+ * process-wide and thread-safe; a destroyed or unknown handle is SV_ERR_ARG.              */
+int sv_bn254_g1_table_create(const sv_g1_affine* bases, size_t n, int form, int device,
+                             uint64_t* handle) SV_NOEXCEPT;
+int sv_bn254_g1_table_destroy(uint64_t handle) SV_NOEXCEPT;
+int sv_bn254_g1_msm_batch_table(uint64_t handle, const uint32_t* base_idx, const sv_fe* scalars,
+                                const uint64_t* offsets, size_t count, int form,
+                                sv_g1_affine* out) SV_NOEXCEPT;
+/* device-buffer form: d_table (table_len rows, `table_form`), d_base_idx / d_scalars / d_offsets /
+ * d_out on `device`; max_terms = the largest MSM (picks the window size); synchronous.        */
+int sv_bn254_g1_msm_batch_indexed_device(const sv_g1_affine* d_table, size_t table_len, int table_form,
+                                         const uint32_t* d_base_idx, const sv_fe* d_scalars,
+                                         const uint64_t* d_offsets, size_t count, size_t max_terms,
+                                         int form, int device, void* stream,
+                                         sv_g1_affine* d_out) SV_NOEXCEPT;
+
 /* ---- Poseidon sponge over BN254 Fr --------------------------
  * x^5 HADES permutation, width t = 3 (R_F 8, R_P 57, rate 2: the SDK's PoseidonTranscript,
  * snark-verifier-sdk/src/halo2.rs:52-71) or t = 5 (R_F 8, R_P 60, rate 4).  States are t

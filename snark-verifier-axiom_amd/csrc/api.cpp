@@ -7,6 +7,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <mutex>
+#include <unordered_map>
 #include <thread>
 #include <vector>
 
@@ -393,6 +395,169 @@ int sv_bn254_g1_msm_batch_device(const sv_g1_affine* d_bases, const sv_fe* d_sca
   SV_HIP(hipSetDevice(device));
   return msm_batch_device(d_bases, d_scalars, d_offsets, nullptr, count, max_terms, form, device, (hipStream_t)stream,
                           d_out);
+  SV_GUARD_END
+}
+
+// ---- fixed-base tables (device-resident constant bases for batched MSMs) -------------------
+namespace {
+struct BaseTable {
+  int dev = 0;
+  void* p = nullptr;
+  size_t n = 0;
+};
+std::mutex g_tables_mu;
+std::unordered_map<uint64_t, BaseTable> g_tables;
+uint64_t g_next_table = 1;
+
+bool table_lookup(uint64_t h, BaseTable* out) {
+  std::lock_guard<std::mutex> lk(g_tables_mu);
+  auto it = g_tables.find(h);
+  if (it == g_tables.end()) return false;
+  *out = it->second;
+  return true;
+}
+
+int check_offsets(const uint64_t* offsets, size_t count) {
+  for (size_t k = 0; k < count; k++) {
+    if (offsets[k + 1] < offsets[k]) {
+      sv::set_error("msm_batch: offsets not non-decreasing at %zu", k);
+      return SV_ERR_ARG;
+    }
+    if (offsets[k + 1] == offsets[k]) {
+      sv::set_error("pairs should not be empty (msm %zu)", k);
+      return SV_ERR_EMPTY;
+    }
+  }
+  return SV_OK;
+}
+}  // namespace
+
+int sv_bn254_g1_table_create(const sv_g1_affine* bases, size_t n, int form, int device, uint64_t* handle) noexcept {
+  SV_GUARD_BEGIN
+  SV_TRY(check_form(form));
+  if (!handle || (!bases && n)) return SV_ERR_ARG;
+  if (n == 0) {
+    sv::set_error("empty base table");
+    return SV_ERR_EMPTY;
+  }
+  if (n > 0xffffffffull) return SV_ERR_LEN;
+  if (resolve_gpus(0) == 0) return SV_ERR_DEVICE;
+  if (device < 0 || device >= runtime_device_count()) {
+    sv::set_error("device %d not initialised", device);
+    return SV_ERR_ARG;
+  }
+  const int dev = runtime_device_id(device);
+  // Montgomery form on the device; coordinates must be reduced (as for every MSM input)
+  std::vector<sv_g1_affine> mont(n);
+  for (size_t i = 0; i < n; i++) {
+    F x, y;
+    memcpy(x.l, bases[i].x.l, 32);
+    memcpy(y.l, bases[i].y.l, 32);
+    if (!sv::host::f_is_reduced(x) || !sv::host::f_is_reduced(y)) {
+      sv::set_error("base table row %zu: coordinate not reduced mod p", i);
+      return SV_ERR_ARG;
+    }
+    const bool ident = sv::host::f_is_zero(x) && sv::host::f_is_zero(y);
+    if (form == SV_CANONICAL && !ident) {
+      x = sv::host::f_to_mont(x);
+      y = sv::host::f_to_mont(y);
+    }
+    memcpy(mont[i].x.l, x.l, 32);
+    memcpy(mont[i].y.l, y.l, 32);
+  }
+  BaseTable t;
+  t.dev = dev;
+  t.n = n;
+  SV_HIP(hipSetDevice(dev));
+  SV_HIP(hipMalloc(&t.p, n * sizeof(sv_g1_affine)));
+  if (hipMemcpy(t.p, mont.data(), n * sizeof(sv_g1_affine), hipMemcpyHostToDevice) != hipSuccess) {
+    hipFree(t.p);
+    sv::set_error("base table upload failed");
+    return SV_ERR_DEVICE;
+  }
+  std::lock_guard<std::mutex> lk(g_tables_mu);
+  *handle = g_next_table++;
+  g_tables[*handle] = t;
+  return SV_OK;
+  SV_GUARD_END
+}
+
+int sv_bn254_g1_table_destroy(uint64_t handle) noexcept {
+  SV_GUARD_BEGIN
+  BaseTable t;
+  {
+    std::lock_guard<std::mutex> lk(g_tables_mu);
+    auto it = g_tables.find(handle);
+    if (it == g_tables.end()) {
+      sv::set_error("unknown base table handle %llu", (unsigned long long)handle);
+      return SV_ERR_ARG;
+    }
+    t = it->second;
+    g_tables.erase(it);
+  }
+  SV_HIP(hipSetDevice(t.dev));
+  SV_HIP(hipFree(t.p));
+  return SV_OK;
+  SV_GUARD_END
+}
+
+int sv_bn254_g1_msm_batch_table(uint64_t handle, const uint32_t* base_idx, const sv_fe* scalars,
+                                const uint64_t* offsets, size_t count, int form, sv_g1_affine* out) noexcept {
+  SV_GUARD_BEGIN
+  SV_TRY(check_form(form));
+  if (count == 0) return SV_OK;
+  if (!offsets || !out) return SV_ERR_ARG;
+  SV_TRY(check_offsets(offsets, count));
+  if (!base_idx || !scalars) return SV_ERR_ARG;
+  if (count > 0x7fffffffull) return SV_ERR_LEN;
+  BaseTable t;
+  if (!table_lookup(handle, &t)) {
+    sv::set_error("unknown base table handle %llu", (unsigned long long)handle);
+    return SV_ERR_ARG;
+  }
+  const uint64_t base = offsets[0], total = offsets[count] - base;
+  size_t max_terms = 0;
+  std::vector<uint64_t> off(offsets, offsets + count + 1);
+  for (auto& o : off) o -= base;
+  for (size_t k = 0; k < count; k++) max_terms = std::max<size_t>(max_terms, off[k + 1] - off[k]);
+  for (uint64_t i = 0; i < total; i++)
+    if (base_idx[base + i] >= t.n) {
+      sv::set_error("msm_batch: base index %u at term %llu out of the table (%zu rows)", base_idx[base + i],
+                    (unsigned long long)(base + i), t.n);
+      return SV_ERR_ARG;
+    }
+  DevBuf didx, ds, doff, dout;
+  SV_TRY(didx.alloc(t.dev, total * sizeof(uint32_t)));
+  SV_TRY(ds.alloc(t.dev, total * sizeof(sv_fe)));
+  SV_TRY(doff.alloc(t.dev, (count + 1) * sizeof(uint64_t)));
+  SV_TRY(dout.alloc(t.dev, count * sizeof(sv_g1_affine)));
+  SV_HIP(hipMemcpy(didx.p, base_idx + base, total * sizeof(uint32_t), hipMemcpyHostToDevice));
+  SV_HIP(hipMemcpy(ds.p, scalars + base, total * sizeof(sv_fe), hipMemcpyHostToDevice));
+  SV_HIP(hipMemcpy(doff.p, off.data(), (count + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
+  SV_TRY(msm_batch_device(t.p, ds.p, static_cast<const uint64_t*>(doff.p), nullptr, count, max_terms, form, t.dev,
+                          nullptr, dout.p, static_cast<const uint32_t*>(didx.p), t.n, SV_MONTGOMERY));
+  SV_HIP(hipMemcpy(out, dout.p, count * sizeof(sv_g1_affine), hipMemcpyDeviceToHost));
+  return SV_OK;
+  SV_GUARD_END
+}
+
+int sv_bn254_g1_msm_batch_indexed_device(const sv_g1_affine* d_table, size_t table_len, int table_form,
+                                         const uint32_t* d_base_idx, const sv_fe* d_scalars,
+                                         const uint64_t* d_offsets, size_t count, size_t max_terms, int form,
+                                         int device, void* stream, sv_g1_affine* d_out) noexcept {
+  SV_GUARD_BEGIN
+  SV_TRY(check_form(form));
+  SV_TRY(check_form(table_form));
+  if (count == 0) return SV_OK;
+  if (!d_table || !d_base_idx || !d_scalars || !d_offsets || !d_out) return SV_ERR_ARG;
+  if (table_len == 0) {
+    sv::set_error("empty base table");
+    return SV_ERR_EMPTY;
+  }
+  if (resolve_gpus(0) == 0) return SV_ERR_DEVICE;
+  SV_HIP(hipSetDevice(device));
+  return msm_batch_device(d_table, d_scalars, d_offsets, nullptr, count, max_terms, form, device,
+                          (hipStream_t)stream, d_out, d_base_idx, table_len, table_form);
   SV_GUARD_END
 }
 

@@ -89,7 +89,9 @@ __global__ void __launch_bounds__(kThreads) k_msm_batch_windows(const G1Aff* __r
                                                                  const Fr* __restrict__ scalars,
                                                                  const uint64_t* __restrict__ off,
                                                                  const uint32_t* __restrict__ ids, int mont,
-                                                                 G1Xyzz* __restrict__ Tg, uint32_t* __restrict__ err) {
+                                                                 G1Xyzz* __restrict__ Tg, uint32_t* __restrict__ err,
+                                                                 const uint32_t* __restrict__ bidx, uint64_t tlen,
+                                                                 int mont_b) {
   using Cf = BatchCfg<C>;
   constexpr int W = Cf::W, B = Cf::B, G = Cf::G, BPL = Cf::BPL, WPB = Cf::WPB, NCH = Cf::NCH;
   __shared__ uint32_t cur[WPB * B];       // histogram, then scatter cursors (= bucket ends)
@@ -184,10 +186,19 @@ __global__ void __launch_bounds__(kThreads) k_msm_batch_windows(const G1Aff* __r
           const uint32_t pe = cur[lw * B + b];
           for (uint32_t p = bst[lw * B + b]; p < pe; p++) {
             const uint32_t e = lst[lw * 2 * NCH + p];
-            const uint32_t* bp = reinterpret_cast<const uint32_t*>(bases + c0 + (e & 0xff));
+            uint64_t bi = c0 + (e & 0xff);
+            if (bidx) {  // base table: term -> table row (fixed bases resident on the device)
+              const uint32_t ti = bidx[bi];
+              if (ti >= tlen) {
+                atomicOr(err, 4u);
+                continue;
+              }
+              bi = ti;
+            }
+            const uint32_t* bp = reinterpret_cast<const uint32_t*>(bases + bi);
             Fq x = ld_fq(bp), y = ld_fq(bp + 8);
             if (x.is_zero() && y.is_zero()) continue;  // identity base
-            if (!mont) {
+            if (!mont_b) {
               x = fe_to_mont(x);
               y = fe_to_mont(y);
             }
@@ -354,7 +365,8 @@ int msm_batch_window_bits(size_t max_terms) {
 }
 
 int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t* d_offsets, const uint32_t* d_ids,
-                     size_t count, size_t max_terms, int form, int device, hipStream_t stream, void* d_out) {
+                     size_t count, size_t max_terms, int form, int device, hipStream_t stream, void* d_out,
+                     const uint32_t* d_bidx, uint64_t table_len, int base_form) {
   if (count == 0) return SV_OK;
   if (count > 0x7fffffffull) {
     set_error("msm_batch: count = %zu too large", count);
@@ -373,15 +385,18 @@ int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t*
   G1Xyzz* Tg = ws->carve<G1Xyzz>(count * W);
   SV_HIP(hipMemsetAsync(err, 0, 4, st));
   const int mont = form == SV_MONTGOMERY;
+  const int mont_b = (d_bidx ? base_form : form) == SV_MONTGOMERY;
   const G1Aff* b = static_cast<const G1Aff*>(d_bases);
   const Fr* s = static_cast<const Fr*>(d_scalars);
   G1Aff* o = static_cast<G1Aff*>(d_out);
   const dim3 grid((uint32_t)count, WG);
   if (c == 5) {
-    hipLaunchKernelGGL(k_msm_batch_windows<5>, grid, dim3(kThreads), 0, st, b, s, d_offsets, d_ids, mont, Tg, err);
+    hipLaunchKernelGGL(k_msm_batch_windows<5>, grid, dim3(kThreads), 0, st, b, s, d_offsets, d_ids, mont, Tg, err,
+                       d_bidx, table_len, mont_b);
     hipLaunchKernelGGL(k_msm_batch_horner<5>, dim3((uint32_t)count), dim3(64), 0, st, Tg, d_ids, mont, o);
   } else {
-    hipLaunchKernelGGL(k_msm_batch_windows<8>, grid, dim3(kThreads), 0, st, b, s, d_offsets, d_ids, mont, Tg, err);
+    hipLaunchKernelGGL(k_msm_batch_windows<8>, grid, dim3(kThreads), 0, st, b, s, d_offsets, d_ids, mont, Tg, err,
+                       d_bidx, table_len, mont_b);
     hipLaunchKernelGGL(k_msm_batch_horner<8>, dim3((uint32_t)count), dim3(64), 0, st, Tg, d_ids, mont, o);
   }
   SV_HIP(hipGetLastError());
@@ -391,6 +406,10 @@ int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t*
   memcpy(&ev, ws->pinned, 4);
   if (ev & 2u) {
     set_error("msm_batch: scalar not reduced (>= r)");
+    return SV_ERR_ARG;
+  }
+  if (ev & 4u) {
+    set_error("msm_batch: base index out of the table (>= %llu)", (unsigned long long)table_len);
     return SV_ERR_ARG;
   }
   return SV_OK;

@@ -9,8 +9,11 @@ namespace sv {
 // count MSMs; MSM k = sum over i in [off[k], off[k+1]) of scalars[i] * bases[i] (device arrays);
 // d_out[k] = affine result in `form`.  max_terms (the largest MSM) only picks the window size.
 // d_ids (optional): launch only MSMs d_ids[0..count) (results still land at d_out[id]).
+// d_bidx (optional): base table mode -- term i uses d_bases[d_bidx[i]] (indices < table_len, else
+// SV_ERR_ARG), the table in `base_form`; scalars and outputs stay in `form`.
 // Synchronous on `stream`.
 int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t* d_offsets, const uint32_t* d_ids,
-                     size_t count, size_t max_terms, int form, int device, hipStream_t stream, void* d_out);
+                     size_t count, size_t max_terms, int form, int device, hipStream_t stream, void* d_out,
+                     const uint32_t* d_bidx = nullptr, uint64_t table_len = 0, int base_form = 0);
 int msm_batch_window_bits(size_t max_terms);
 }  // namespace sv

@@ -10,7 +10,7 @@ All compute runs in libsvgpu.so (HIP, gfx950); there is no CPU fallback.
 from ._lib import (SV_CANONICAL, SV_MONTGOMERY, ArgumentError, DeviceError, EmptyError, LengthError,
                    OutOfMemoryError, SvError, lib)
 from .kzg import AssertionFailure, KzgAccumulator, KzgAs, KzgDecidingKey
-from .loader import (NativeLoader, ReferencePanic, batch_multi_scalar_multiplication, fold_partials, msm_arrays,
+from .loader import (BaseTable, NativeLoader, ReferencePanic, batch_multi_scalar_multiplication, fold_partials, msm_arrays,
                      msm_batch_arrays, multi_scalar_multiplication)
 
 

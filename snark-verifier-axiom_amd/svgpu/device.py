@@ -126,3 +126,20 @@ def msm_batch(bases: torch.Tensor, scalars: torch.Tensor, offsets: torch.Tensor,
                                                      out.data_ptr()),
                "sv_bn254_g1_msm_batch_device")
     return out[:count]
+
+
+def msm_batch_indexed(table: torch.Tensor, base_idx: torch.Tensor, scalars: torch.Tensor, offsets: torch.Tensor,
+                      max_terms: int, form: int = _lib.SV_MONTGOMERY, table_form: int = _lib.SV_MONTGOMERY,
+                      out: torch.Tensor = None) -> torch.Tensor:
+    """Batched MSMs whose terms reference rows of an HBM-resident base table (table: (rows, 8) int64;
+    base_idx: (terms,) int32 row indices; offsets: (count + 1,) int64); returns (count, 8) int64."""
+    count = offsets.shape[0] - 1
+    if out is None:
+        out = torch.empty((max(count, 1), 8), dtype=torch.int64, device=scalars.device)
+    d = _dev_index(scalars)
+    _lib.check(_lib.lib.sv_bn254_g1_msm_batch_indexed_device(table.data_ptr(), table.shape[0], table_form,
+                                                             base_idx.data_ptr(), scalars.data_ptr(),
+                                                             offsets.data_ptr(), count, max_terms, form, d,
+                                                             _stream_handle(scalars.device), out.data_ptr()),
+               "sv_bn254_g1_msm_batch_indexed_device")
+    return out[:count]

@@ -73,6 +73,78 @@ def msm_batch_arrays(bases: np.ndarray, scalars: np.ndarray, offsets: Sequence[i
     return [enc.g1_from_struct(o, form) for o in out]
 
 
+class BaseTable:
+    """Device-resident fixed bases (the generator and a circuit's preprocessed commitments, loaded
+    once per verifier: Protocol::loaded, plonk/protocol.rs:106-131) referenced by row index from
+    each proof's MSMs (Msm::evaluate, bdfg21.rs:75-78 / gwc19.rs:76-79), so a per-proof batch ships
+    only scalars and u32 indices.  Rows are uploaded once in Montgomery form on `device`."""
+
+    def __init__(self, bases, device: int = 0):
+        if not isinstance(bases, np.ndarray):
+            bases = enc.bases_array(list(bases))
+        arr = np.ascontiguousarray(bases, dtype=np.uint64)
+        self.n = arr.shape[0]
+        self.handle = None
+        h = ctypes.c_uint64(0)
+        _lib.check(_lib.lib.sv_bn254_g1_table_create(arr.ctypes.data, self.n, _lib.SV_CANONICAL, device,
+                                                     ctypes.byref(h)), "sv_bn254_g1_table_create")
+        self.handle = h.value
+
+    def close(self):
+        if self.handle is not None:
+            h, self.handle = self.handle, None
+            _lib.check(_lib.lib.sv_bn254_g1_table_destroy(h), "sv_bn254_g1_table_destroy")
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def msm_batch_arrays(self, base_idx: np.ndarray, scalars: np.ndarray, offsets: Sequence[int],
+                         form: int = _lib.SV_CANONICAL) -> list:
+        """MSM k = sum over i in [offsets[k], offsets[k+1]) of scalars[i] * table[base_idx[i]]."""
+        if self.handle is None:
+            raise _lib.ArgumentError("base table is closed")
+        idx = np.ascontiguousarray(base_idx, dtype=np.uint32)
+        scalars = np.ascontiguousarray(scalars, dtype=np.uint64)
+        if idx.shape[0] != scalars.shape[0]:
+            raise ReferencePanic("assertion failed: scalars.len() == bases.len()")
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        count = off.shape[0] - 1
+        if count <= 0:
+            return []
+        if int(off[-1]) > idx.shape[0]:
+            raise _lib.LengthError("msm_batch: offsets run past the arrays")
+        out = (_lib.sv_g1_affine * count)()
+        rc = _lib.lib.sv_bn254_g1_msm_batch_table(self.handle, idx.ctypes.data, scalars.ctypes.data,
+                                                  off.ctypes.data, count, form, ctypes.cast(out, ctypes.c_void_p))
+        if rc == _lib.SV_ERR_EMPTY:
+            raise ReferencePanic("pairs should not be empty")
+        _lib.check(rc, "sv_bn254_g1_msm_batch_table")
+        return [enc.g1_from_struct(o, form) for o in out]
+
+    def batch_multi_scalar_multiplication(self, msms: Sequence[Sequence[Tuple[int, int]]]) -> list:
+        """msms: per MSM a list of (scalar, table row) pairs."""
+        offsets = [0]
+        scalars, idx = [], []
+        for pairs in msms:
+            if len(pairs) == 0:
+                raise ReferencePanic("pairs should not be empty")
+            scalars += [s for s, _ in pairs]
+            idx += [i for _, i in pairs]
+            offsets.append(len(scalars))
+        if not msms:
+            return []
+        return self.msm_batch_arrays(np.array(idx, dtype=np.uint32), enc.scalars_array(scalars), offsets)
+
+
 def batch_multi_scalar_multiplication(msms: Sequence[Sequence[Tuple[int, Point]]]) -> list:
     """[NativeLoader.multi_scalar_multiplication(pairs) for pairs in msms], one GPU launch."""
     offsets = [0]

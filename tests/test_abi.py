@@ -116,6 +116,30 @@ def test_msm_batch_arguments_rejected_without_compute():
     assert svgpu.batch_multi_scalar_multiplication([]) == []
 
 
+def test_base_table_arguments_rejected_without_compute():
+    from svgpu import _lib
+    buf = np.zeros(64, np.uint64)
+    h = ctypes.c_uint64(0)
+    assert _lib.lib.sv_bn254_g1_table_create(buf.ctypes.data, 0, 0, 0, ctypes.byref(h)) == _lib.SV_ERR_EMPTY
+    assert _lib.lib.sv_bn254_g1_table_create(buf.ctypes.data, 1, 9, 0, ctypes.byref(h)) == _lib.SV_ERR_ARG
+    assert _lib.lib.sv_bn254_g1_table_create(None, 1, 0, 0, ctypes.byref(h)) == _lib.SV_ERR_ARG
+    assert _lib.lib.sv_bn254_g1_table_destroy(123456789) == _lib.SV_ERR_ARG
+    assert "unknown base table" in _lib.last_error()
+    idx = np.zeros(4, np.uint32)
+    bad = np.array([0, 2, 1], np.uint64)
+    empty = np.array([0, 1, 1], np.uint64)
+    good = np.array([0, 1, 2], np.uint64)
+    out = np.zeros(64, np.uint64)
+    call = _lib.lib.sv_bn254_g1_msm_batch_table
+    assert call(1, idx.ctypes.data, buf.ctypes.data, bad.ctypes.data, 2, 0, out.ctypes.data) == _lib.SV_ERR_ARG
+    assert call(1, idx.ctypes.data, buf.ctypes.data, empty.ctypes.data, 2, 0, out.ctypes.data) == _lib.SV_ERR_EMPTY
+    assert call(987654, idx.ctypes.data, buf.ctypes.data, good.ctypes.data, 2, 0, out.ctypes.data) == _lib.SV_ERR_ARG
+    assert call(1, None, None, None, 0, 0, None) == _lib.SV_OK
+    dev = _lib.lib.sv_bn254_g1_msm_batch_indexed_device
+    assert dev(buf.ctypes.data, 0, 0, idx.ctypes.data, buf.ctypes.data, good.ctypes.data, 2, 1, 0, 0, None,
+               out.ctypes.data) == _lib.SV_ERR_EMPTY
+
+
 def test_codec_arguments_rejected_without_compute():
     from svgpu import _lib
     buf = np.zeros(64, np.uint8)

@@ -108,3 +108,60 @@ def test_device_api_config5_shape(gpu, oracle_cpp):
     B = oracle_cpp.gen_bases(b.SEED_BASES, n)
     S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n)
     assert got == _expected(oracle_cpp, B, S, list(range(0, n + 1, m)))
+
+
+def test_base_table_host_api(gpu, oracle_cpp):
+    """Fixed bases uploaded once, referenced by index from ragged per-proof MSMs (repeated rows,
+    identity row, both windows' sizes); then an out-of-table index and a destroyed handle."""
+    import svgpu
+    T = oracle_cpp.gen_bases(b.SEED_BASES, 300, start=4242)
+    T[7] = 0                                           # identity row
+    rng = np.random.default_rng(11)
+    sizes = [1, 3, 64, 65, 129, 300, 700]
+    n = sum(sizes)
+    idx = rng.integers(0, 300, n).astype(np.uint32)
+    S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=4242)
+    off = [0]
+    for m in sizes:
+        off.append(off[-1] + m)
+    with svgpu.BaseTable(T) as tab:
+        got = tab.msm_batch_arrays(idx, S, off)
+        assert got == _expected(oracle_cpp, T[idx], S, off)
+        with pytest.raises(svgpu.ArgumentError):
+            tab.msm_batch_arrays(np.array([300], np.uint32), S[:1], [0, 1])
+        pairs = [[(5, 1), (7, 2)], [(b.R - 1, 3), (1, 3)]]
+        from svgpu import encoding as enc
+        assert tab.batch_multi_scalar_multiplication(pairs) == [
+            b.native_msm([s for s, _ in p], [enc.g1_from_limbs(T[i]) for _, i in p]) for p in pairs]
+        h = tab.handle
+    from svgpu import _lib
+    out = np.zeros(8, np.uint64)
+    assert _lib.lib.sv_bn254_g1_msm_batch_table(h, idx.ctypes.data, S.ctypes.data,
+                                                np.array([0, 1], np.uint64).ctypes.data, 1, 0,
+                                                out.ctypes.data) == _lib.SV_ERR_ARG
+
+
+def test_indexed_device_api_matches_direct(gpu, oracle_cpp):
+    """Device-buffer table form: a 64-row table referenced by 128 MSMs of 64 terms equals the
+    direct batch over the gathered bases; an out-of-range index is caught on the device."""
+    import svgpu
+    from svgpu import device as dv
+    rows, count, m = 64, 128, 64
+    n = count * m
+    T = dv.gen_bases(dv.empty_bases(rows, gpu), b.SEED_BASES, 0, svgpu.SV_MONTGOMERY)
+    Sd = dv.gen_scalars(dv.empty_scalars(n, gpu), b.SEED_SCALARS, 0, svgpu.SV_MONTGOMERY)
+    idx = torch.randint(0, rows, (n,), dtype=torch.int32, device=gpu, generator=None)
+    off = torch.arange(0, n + 1, m, dtype=torch.int64, device=gpu)
+    got = dv.msm_batch_indexed(T, idx, Sd, off, m)
+    ref = dv.msm_batch(T[idx.long()].contiguous(), Sd, off, m)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    from svgpu import encoding as enc
+    Th = oracle_cpp.gen_bases(b.SEED_BASES, rows)
+    Sh = oracle_cpp.gen_scalars(b.SEED_SCALARS, n)
+    ih = idx.cpu().numpy()
+    exp = _expected(oracle_cpp, Th[ih[:4 * m]], Sh[:4 * m], list(range(0, 4 * m + 1, m)))
+    assert [enc.g1_from_limbs(r, svgpu.SV_MONTGOMERY) for r in got[:4].cpu().numpy().view(np.uint64)] == exp
+    idx[5] = rows
+    with pytest.raises(svgpu.ArgumentError):
+        dv.msm_batch_indexed(T, idx, Sd, off, m)

@@ -678,9 +678,28 @@ __global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, c
   uint32_t lo = j * L;
   uint32_t hi = min(N, lo + L);
   G1Xyzz run = G1Xyzz::identity(), acc = G1Xyzz::identity();
-  for (uint32_t i = hi; i-- > lo;) {
-    if (gs[i] != gs[i + 1]) run = xyzz_add(run, load_xyzz(x, i));
-    if (base || i > lo) acc = xyzz_add(acc, run);
+  if (hi > lo) {
+    // bucket i - 1 (and its emptiness) is loaded while bucket i is being added (A/B at 2^20:
+    // reduce 0.404 -> 0.393 ms)
+    uint32_t i = hi - 1;
+    uint32_t gn = gs[i + 1], g0 = gs[i];
+    bool ne = g0 != gn;
+    G1Xyzz nx = ne ? load_xyzz(x, i) : G1Xyzz::identity();
+    for (;;) {
+      const G1Xyzz cur = nx;
+      const bool cne = ne;
+      const uint32_t ci = i;
+      if (ci > lo) {
+        i = ci - 1;
+        gn = g0;
+        g0 = gs[i];
+        ne = g0 != gn;
+        if (ne) nx = load_xyzz(x, i);
+      }
+      if (cne) run = xyzz_add(run, cur);
+      if (base || ci > lo) acc = xyzz_add(acc, run);
+      if (ci == lo) break;
+    }
   }
   store_xyzz(acc_out, tid, acc);
   if (tot_out) store_xyzz(tot_out, tid, run);

@@ -76,6 +76,13 @@ def next_rows(dev, dv, ob, enc, g2, sg2, accs):
     off = torch.arange(0, count * m + 1, m, dtype=torch.int64, device=dev)
     t, _ = _time(lambda: dv.msm_batch(B, S, off, m, M), 5)
     res["msm_batch"] = {"msms": count, "terms_each": m, "ms": t * 1e3, "terms_per_s": count * m / t}
+    # f1 with fixed bases: the same batch, each term referencing a row of a 4096-row device table
+    rows = 4096
+    T = dv.gen_bases(dv.empty_bases(rows, dev), ob.SEED_BASES, 0, M)
+    idx = torch.randint(0, rows, (count * m,), dtype=torch.int32, device=dev)
+    t, _ = _time(lambda: dv.msm_batch_indexed(T, idx, S, off, m, M, M), 5)
+    res["msm_batch_table"] = {"msms": count, "terms_each": m, "table_rows": rows, "ms": t * 1e3,
+                              "terms_per_s": count * m / t}
     # config 5: 64 valid accumulators -> KzgAs::create_proof MSMs (r^0..r^63) -> one decide
     acc64 = accs[:64]
     r = ob.gen_scalar(ob.SEED_SCALARS, 1 << 30)

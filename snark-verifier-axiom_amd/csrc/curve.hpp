@@ -34,12 +34,12 @@ struct G1Xyzz {
 SV_HD G1Xyzz xyzz_dbl(const G1Xyzz& p) {
   if (p.is_identity()) return p;
   Fq U = fe_dbl(p.Y);
-  Fq V = fe_sqr(U);
+  Fq V = fe_sqr_hp(U);
   Fq W = U * V;
   Fq S = p.X * V;
-  Fq X2 = fe_sqr(p.X);
+  Fq X2 = fe_sqr_hp(p.X);
   Fq M = fe_dbl(X2) + X2;
-  Fq X3 = fe_sqr(M) - fe_dbl(S);
+  Fq X3 = fe_sqr_hp(M) - fe_dbl(S);
   Fq Y3 = M * (S - X3) - W * p.Y;
   return {X3, Y3, V * p.ZZ, W * p.ZZZ};
 }
@@ -47,12 +47,12 @@ SV_HD G1Xyzz xyzz_dbl(const G1Xyzz& p) {
 // mdbl-2008-s-1: double an affine point (not identity)
 SV_HD G1Xyzz xyzz_mdbl(const Fq& x, const Fq& y) {
   Fq U = fe_dbl(y);
-  Fq V = fe_sqr(U);
+  Fq V = fe_sqr_hp(U);
   Fq W = U * V;
   Fq S = x * V;
-  Fq X2 = fe_sqr(x);
+  Fq X2 = fe_sqr_hp(x);
   Fq M = fe_dbl(X2) + X2;
-  Fq X3 = fe_sqr(M) - fe_dbl(S);
+  Fq X3 = fe_sqr_hp(M) - fe_dbl(S);
   Fq Y3 = M * (S - X3) - W * y;
   return {X3, Y3, V, W};
 }
@@ -68,10 +68,10 @@ SV_HD G1Xyzz xyzz_madd(const G1Xyzz& p, const Fq& x2, const Fq& y2) {
     if (Rd.is_zero()) return xyzz_mdbl(x2, y2);
     return G1Xyzz::identity();
   }
-  Fq PP = fe_sqr(Pd);
+  Fq PP = fe_sqr_hp(Pd);
   Fq PPP = Pd * PP;
   Fq Q = p.X * PP;
-  Fq X3 = fe_sqr(Rd) - PPP - fe_dbl(Q);
+  Fq X3 = fe_sqr_hp(Rd) - PPP - fe_dbl(Q);
   Fq Y3 = Rd * (Q - X3) - p.Y * PPP;
   return {X3, Y3, p.ZZ * PP, p.ZZZ * PPP};
 }
@@ -95,10 +95,10 @@ SV_HD G1Xyzz xyzz_add(const G1Xyzz& p, const G1Xyzz& q) {
     if (Rd.is_zero()) return xyzz_dbl(p);
     return G1Xyzz::identity();
   }
-  Fq PP = fe_sqr(Pd);
+  Fq PP = fe_sqr_hp(Pd);
   Fq PPP = Pd * PP;
   Fq Q = U1 * PP;
-  Fq X3 = fe_sqr(Rd) - PPP - fe_dbl(Q);
+  Fq X3 = fe_sqr_hp(Rd) - PPP - fe_dbl(Q);
   Fq Y3 = Rd * (Q - X3) - S1 * PPP;
   return {X3, Y3, p.ZZ * q.ZZ * PP, p.ZZZ * q.ZZZ * PPP};
 }

@@ -392,6 +392,134 @@ SV_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
 }
 #endif
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// Montgomery squaring for throughput-bound code (many waves per SIMD: bucket accumulation, Poseidon):
+// the 28 off-diagonal products a_i a_j (i < j) are scanned once into a 512-bit
+// half product, doubled by one funnel shift per word, and folded into the same product-scanning
+// Montgomery pass as operator* with the 8 diagonal squares (100 instead of 128 v_mad_u64_u32).
+// The column carry entering the main pass stays below 2^36 (at most 9 products per column), so
+// adding a doubled word cannot overflow the 64-bit accumulator.  Measured: k_accumulate 1.52 ->
+// 1.49 ms at 2^20; single-wave chains (decider, batched Horner) were ~1 % slower with it (two
+// dependent scans), so fe_sqr stays a * a and only the XYZZ formulas and Poseidon use fe_sqr_hp.
+template <class M>
+SV_HD Fe<M> fe_sqr_hp(const Fe<M>& a) {
+  uint32_t od[16];
+  uint64_t acc = 0;
+  uint32_t ovf = 0;
+  od[0] = 0;
+#pragma unroll
+  for (int k = 1; k < 14; k++) {
+    uint32_t xs[4], ys[4];
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int j = k - i;
+      if (i < j && j < 8) {
+        xs[c] = a.v[i];
+        ys[c] = a.v[j];
+        c++;
+      }
+    }
+    int q;
+    if (c >= 4) {
+      mac_first4(acc, ovf, xs, ys);
+      q = 4;
+    } else if (c >= 2) {
+      mac_first2(acc, ovf, xs[0], ys[0], xs[1], ys[1]);
+      q = 2;
+    } else {
+      mac_first(acc, ovf, xs[0], ys[0]);
+      q = 1;
+    }
+#pragma unroll
+    for (; q + 1 < c; q += 2) mac_carry2(acc, ovf, xs[q], ys[q], xs[q + 1], ys[q + 1]);
+#pragma unroll
+    for (; q < c; q++) mac_carry(acc, ovf, xs[q], ys[q]);
+    od[k] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)ovf << 32);
+  }
+  od[14] = (uint32_t)acc;
+  od[15] = (uint32_t)(acc >> 32);
+  uint32_t d[16];
+  d[0] = 0;
+#pragma unroll
+  for (int k = 1; k < 16; k++) d[k] = __builtin_amdgcn_alignbit(od[k], od[k - 1], 31);
+
+  uint32_t m[8], t[8];
+  acc = 0;
+  ovf = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    acc += d[k];
+    uint32_t xs[9], ys[9];
+    int c = 0;
+    if ((k & 1) == 0 && k < 16) {
+      xs[c] = a.v[k >> 1];
+      ys[c] = a.v[k >> 1];
+      c++;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < 8) {
+        xs[c] = m[i];
+        ys[c] = M::p(j);
+        c++;
+      }
+    }
+    int q = 0;
+    bool open = false;
+    if (c >= 4) {
+      mac_first4(acc, ovf, xs, ys);
+      q = 4;
+      open = true;
+    } else if (c >= 2) {
+      mac_first2(acc, ovf, xs[0], ys[0], xs[1], ys[1]);
+      q = 2;
+      open = true;
+    } else if (c == 1) {
+      mac_first(acc, ovf, xs[0], ys[0]);
+      q = 1;
+      open = true;
+    }
+#pragma unroll
+    for (; q + 3 < c; q += 4) mac_carry4(acc, ovf, xs + q, ys + q);
+#pragma unroll
+    for (; q + 1 < c; q += 2) mac_carry2(acc, ovf, xs[q], ys[q], xs[q + 1], ys[q + 1]);
+#pragma unroll
+    for (; q < c; q++) mac_carry(acc, ovf, xs[q], ys[q]);
+    if (k < 8) {
+      m[k] = (uint32_t)acc * M::NP0;
+      if (open) mac_carry(acc, ovf, m[k], M::p(0));
+      else mac_first(acc, ovf, m[k], M::p(0));
+    } else {
+      t[k - 8] = (uint32_t)acc;
+      if (!open) ovf = 0;
+    }
+    acc = (acc >> 32) | ((uint64_t)ovf << 32);
+  }
+  const uint32_t top = (uint32_t)acc;
+  Fe<M> dd;
+  uint64_t br = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    uint64_t s = (uint64_t)t[j] - M::p(j) - br;
+    dd.v[j] = (uint32_t)s;
+    br = (s >> 63) & 1;
+  }
+  const bool ge = (top != 0) || (br == 0);
+  Fe<M> r;
+#pragma unroll
+  for (int j = 0; j < 8; j++) r.v[j] = ge ? dd.v[j] : t[j];
+  return r;
+}
+#else
+template <class M>
+SV_HD Fe<M> fe_sqr_hp(const Fe<M>& a) {
+  return a * a;
+}
+#endif
+
 template <class M>
 SV_HD Fe<M> fe_sqr(const Fe<M>& a) {
   return a * a;

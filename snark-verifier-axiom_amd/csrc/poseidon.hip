@@ -44,8 +44,8 @@ __device__ __forceinline__ Fr ld_const(const uint32_t* p) {
 }
 
 __device__ __forceinline__ Fr pow5(const Fr& x) {
-  const Fr x2 = fe_sqr(x);
-  return fe_sqr(x2) * x;
+  const Fr x2 = fe_sqr_hp(x);
+  return fe_sqr_hp(x2) * x;
 }
 
 // poseidon.rs:121-161 (permutation) == tests.rs's HADES reference: R_F/2 full, R_P partial, R_F/2 full.

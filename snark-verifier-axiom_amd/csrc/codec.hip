@@ -70,7 +70,7 @@ __global__ void k_decode_compressed(const uint8_t* __restrict__ in, uint32_t n, 
   Fq y = Fq::one();
   for (int li = 7; li >= 0; li--)
     for (int b = 31; b >= 0; b--) {
-      y = fe_sqr(y);
+      y = fe_sqr_hp(y);
       if ((FQ_SQRT_EXP[li] >> b) & 1) y = y * rhs;
     }
   if (fe_sqr(y) != rhs) {

@@ -525,6 +525,96 @@ SV_HD Fe<M> fe_sqr(const Fe<M>& a) {
   return a * a;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// Sum of N Montgomery products with ONE reduction: column k of the product scan accumulates
+// a_n,i b_n,k-i for every pair n and then m_i p_k-i, so N products cost 64 N + 64 multiply-adds
+// instead of 128 N.  With p < 2^254 the scanned value is below (N p^2 + 2^256 p) / 2^256 < 2p for
+// N <= 3, so the single conditional subtraction of operator* still reduces fully.
+template <class M, int N>
+SV_HD Fe<M> fe_mul_sum(const Fe<M> (&a)[N], const Fe<M> (&b)[N]) {
+  static_assert(N >= 1 && N <= 3, "fe_mul_sum: the final subtraction covers N <= 3");
+  uint32_t m[8], t[8];
+  uint64_t acc = 0;
+  uint32_t ovf = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    uint32_t xs[8 * N + 8], ys[8 * N + 8];
+    int c = 0;
+#pragma unroll
+    for (int n = 0; n < N; n++)
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const int j = k - i;
+        if (j >= 0 && j < 8) {
+          xs[c] = a[n].v[i];
+          ys[c] = b[n].v[j];
+          c++;
+        }
+      }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < 8) {
+        xs[c] = m[i];
+        ys[c] = M::p(j);
+        c++;
+      }
+    }
+    int q = 0;
+    bool open = false;
+    if (c >= 4) {
+      mac_first4(acc, ovf, xs, ys);
+      q = 4;
+      open = true;
+    } else if (c >= 2) {
+      mac_first2(acc, ovf, xs[0], ys[0], xs[1], ys[1]);
+      q = 2;
+      open = true;
+    } else if (c == 1) {
+      mac_first(acc, ovf, xs[0], ys[0]);
+      q = 1;
+      open = true;
+    }
+#pragma unroll
+    for (; q + 3 < c; q += 4) mac_carry4(acc, ovf, xs + q, ys + q);
+#pragma unroll
+    for (; q + 1 < c; q += 2) mac_carry2(acc, ovf, xs[q], ys[q], xs[q + 1], ys[q + 1]);
+#pragma unroll
+    for (; q < c; q++) mac_carry(acc, ovf, xs[q], ys[q]);
+    if (k < 8) {
+      m[k] = (uint32_t)acc * M::NP0;
+      if (open) mac_carry(acc, ovf, m[k], M::p(0));
+      else mac_first(acc, ovf, m[k], M::p(0));
+    } else {
+      t[k - 8] = (uint32_t)acc;
+      if (!open) ovf = 0;
+    }
+    acc = (acc >> 32) | ((uint64_t)ovf << 32);
+  }
+  const uint32_t top = (uint32_t)acc;
+  Fe<M> d;
+  uint64_t br = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    uint64_t s = (uint64_t)t[j] - M::p(j) - br;
+    d.v[j] = (uint32_t)s;
+    br = (s >> 63) & 1;
+  }
+  const bool ge = (top != 0) || (br == 0);
+  Fe<M> r;
+#pragma unroll
+  for (int j = 0; j < 8; j++) r.v[j] = ge ? d.v[j] : t[j];
+  return r;
+}
+#else
+template <class M, int N>
+SV_HD Fe<M> fe_mul_sum(const Fe<M> (&a)[N], const Fe<M> (&b)[N]) {
+  Fe<M> r = a[0] * b[0];
+  for (int n = 1; n < N; n++) r = r + a[n] * b[n];
+  return r;
+}
+#endif
+
 template <class M>
 SV_HD Fe<M> fe_to_mont(const Fe<M>& a) {
   Fe<M> r2;

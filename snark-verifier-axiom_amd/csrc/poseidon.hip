@@ -48,6 +48,26 @@ __device__ __forceinline__ Fr pow5(const Fr& x) {
   return fe_sqr_hp(x2) * x;
 }
 
+// One MDS row, sum_j s_j M_ij, as fused sums of up to three products with one Montgomery reduction
+// each (fe_mul_sum): t = 3 is one reduction per row instead of three.
+template <int T>
+__device__ __forceinline__ Fr mds_row(const Fr (&s)[T], const uint32_t* row) {
+  constexpr int A = T < 3 ? T : 3;
+  Fr x[A], y[A];
+#pragma unroll
+  for (int j = 0; j < A; j++) x[j] = s[j], y[j] = ld_const(row + j * 8);
+  Fr acc = fe_mul_sum(x, y);
+  if constexpr (T > 3) {
+    constexpr int B = T - 3;
+    static_assert(B <= 3, "mds_row: t <= 6");
+    Fr u[B], v[B];
+#pragma unroll
+    for (int j = 0; j < B; j++) u[j] = s[3 + j], v[j] = ld_const(row + (3 + j) * 8);
+    acc = acc + fe_mul_sum(u, v);
+  }
+  return acc;
+}
+
 // poseidon.rs:121-161 (permutation) == tests.rs's HADES reference: R_F/2 full, R_P partial, R_F/2 full.
 template <int T>
 __device__ __forceinline__ void permute(Fr (&s)[T]) {
@@ -65,12 +85,7 @@ __device__ __forceinline__ void permute(Fr (&s)[T]) {
     }
     Fr o[T];
 #pragma unroll
-    for (int i = 0; i < T; i++) {
-      Fr acc = s[0] * ld_const(mds + (i * T) * 8);
-#pragma unroll
-      for (int j = 1; j < T; j++) acc = acc + s[j] * ld_const(mds + (i * T + j) * 8);
-      o[i] = acc;
-    }
+    for (int i = 0; i < T; i++) o[i] = mds_row<T>(s, mds + i * T * 8);
 #pragma unroll
     for (int i = 0; i < T; i++) s[i] = o[i];
   }

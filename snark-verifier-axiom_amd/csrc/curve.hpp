@@ -30,6 +30,14 @@ struct G1Xyzz {
   }
 };
 
+// a b - c d with one Montgomery reduction (fe_mul_sum over (a, c) x (b, -d)): the Y3 of every
+// XYZZ formula, 192 instead of 256 multiply-adds.
+SV_HD Fq mul_diff(const Fq& a, const Fq& b, const Fq& c, const Fq& d) {
+  const Fq x[2] = {a, c};
+  const Fq y[2] = {b, -d};
+  return fe_mul_sum(x, y);
+}
+
 // dbl-2008-s-1 (a = 0)
 SV_HD G1Xyzz xyzz_dbl(const G1Xyzz& p) {
   if (p.is_identity()) return p;
@@ -40,7 +48,7 @@ SV_HD G1Xyzz xyzz_dbl(const G1Xyzz& p) {
   Fq X2 = fe_sqr_hp(p.X);
   Fq M = fe_dbl(X2) + X2;
   Fq X3 = fe_sqr_hp(M) - fe_dbl(S);
-  Fq Y3 = M * (S - X3) - W * p.Y;
+  Fq Y3 = mul_diff(M, S - X3, W, p.Y);
   return {X3, Y3, V * p.ZZ, W * p.ZZZ};
 }
 
@@ -53,7 +61,7 @@ SV_HD G1Xyzz xyzz_mdbl(const Fq& x, const Fq& y) {
   Fq X2 = fe_sqr_hp(x);
   Fq M = fe_dbl(X2) + X2;
   Fq X3 = fe_sqr_hp(M) - fe_dbl(S);
-  Fq Y3 = M * (S - X3) - W * y;
+  Fq Y3 = mul_diff(M, S - X3, W, y);
   return {X3, Y3, V, W};
 }
 
@@ -72,7 +80,7 @@ SV_HD G1Xyzz xyzz_madd(const G1Xyzz& p, const Fq& x2, const Fq& y2) {
   Fq PPP = Pd * PP;
   Fq Q = p.X * PP;
   Fq X3 = fe_sqr_hp(Rd) - PPP - fe_dbl(Q);
-  Fq Y3 = Rd * (Q - X3) - p.Y * PPP;
+  Fq Y3 = mul_diff(Rd, Q - X3, p.Y, PPP);
   return {X3, Y3, p.ZZ * PP, p.ZZZ * PPP};
 }
 
@@ -99,7 +107,7 @@ SV_HD G1Xyzz xyzz_add(const G1Xyzz& p, const G1Xyzz& q) {
   Fq PPP = Pd * PP;
   Fq Q = U1 * PP;
   Fq X3 = fe_sqr_hp(Rd) - PPP - fe_dbl(Q);
-  Fq Y3 = Rd * (Q - X3) - S1 * PPP;
+  Fq Y3 = mul_diff(Rd, Q - X3, S1, PPP);
   return {X3, Y3, p.ZZ * q.ZZ * PP, p.ZZZ * q.ZZZ * PPP};
 }
 

@@ -297,6 +297,10 @@ int sv_bn254_kzg_accumulate(const sv_g1_affine* lhs, const sv_g1_affine* rhs, si
     return SV_ERR_ARG;
   }
   SV_TRY(check_form(form));
+  if (!host::f_is_reduced(fe_in(*r), host::R64)) {
+    sv::set_error("r not reduced mod the scalar field order");
+    return SV_ERR_ARG;
+  }
   if (resolve_gpus(1) == 0) return SV_ERR_DEVICE;
   int dev = runtime_device_id(0);
   DevBuf dbl, dbr, dsc, drr;

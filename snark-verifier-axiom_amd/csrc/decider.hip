@@ -12,6 +12,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -559,16 +560,34 @@ __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ l
 }
 
 // ---------------------------------------------------------------------------------------------
-// Host side: prepared-line cache (one entry per device: the deciding key rarely changes).
+// Host side: prepared-line cache.  Each deciding key's lines live in their own immutable device
+// buffer, shared by refcount: a call holds its entry until its stream has synchronised, so a
+// concurrent call with another key (a second verifier on another rayon worker) uploads into a NEW
+// buffer and can never overwrite lines a running kernel reads.  A few keys are kept per device
+// (verifiers rarely switch keys); an evicted entry is freed when its last in-flight call drops it.
 // ---------------------------------------------------------------------------------------------
 namespace {
+struct LineEntry {
+  unsigned char key[2 * sizeof(G2Aff)];
+  int device = 0;
+  LineCoeff* d_lines = nullptr;  // 2 * ATE_NUM_LINES, written once before the entry is published
+  ~LineEntry() {
+    if (d_lines) {
+      int prev = 0;
+      (void)hipGetDevice(&prev);
+      (void)hipSetDevice(device);
+      (void)hipFree(d_lines);
+      (void)hipSetDevice(prev);
+    }
+  }
+};
+constexpr int kLineCacheKeys = 4;
 struct LineCache {
   std::mutex mu;
-  bool valid = false;
-  unsigned char key[2 * sizeof(G2Aff)];
-  LineCoeff* d_lines = nullptr;  // 2 * ATE_NUM_LINES
+  std::shared_ptr<LineEntry> e[kLineCacheKeys];  // most recently used first
 };
-LineCache g_cache[64];
+// leaked on purpose: cached entries must not hipFree from static destructors after HIP teardown
+LineCache* const g_cache = new LineCache[64];
 }  // namespace
 
 static G2Aff g2_from_abi(const sv_g2_affine* q, int mont_in) {
@@ -592,8 +611,9 @@ static bool g2_on_twist(const G2Aff& q) {
   return lhs == rhs;
 }
 
-int decider_lines(const sv_g2_affine* g2, const sv_g2_affine* s_g2, int form, int device,
-                  hipStream_t st, const LineCoeff** out) {
+// The caller keeps `*out` alive until every kernel reading its lines has finished.
+static int decider_lines(const sv_g2_affine* g2, const sv_g2_affine* s_g2, int form, int device,
+                         hipStream_t st, std::shared_ptr<LineEntry>* out) {
   if (device < 0 || device >= 64) return SV_ERR_ARG;
   G2Aff q1 = g2_from_abi(g2, form == SV_MONTGOMERY);
   G2Aff q2 = g2_from_abi(s_g2, form == SV_MONTGOMERY);
@@ -602,24 +622,38 @@ int decider_lines(const sv_g2_affine* g2, const sv_g2_affine* s_g2, int form, in
     return SV_ERR_ARG;
   }
   q2.y = -q2.y;  // -s_g2
-  LineCache& c = g_cache[device];
-  std::lock_guard<std::mutex> lk(c.mu);
-  unsigned char key[sizeof c.key];
+  unsigned char key[sizeof(LineEntry::key)];
   memcpy(key, &q1, sizeof(G2Aff));
   memcpy(key + sizeof(G2Aff), &q2, sizeof(G2Aff));
-  if (c.valid && memcmp(key, c.key, sizeof key) == 0) {
-    *out = c.d_lines;
-    return SV_OK;
+  LineCache& c = g_cache[device];
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    for (int i = 0; i < kLineCacheKeys; i++) {
+      if (c.e[i] && memcmp(key, c.e[i]->key, sizeof key) == 0) {
+        std::shared_ptr<LineEntry> hit = c.e[i];
+        for (int j = i; j > 0; j--) c.e[j] = c.e[j - 1];
+        c.e[0] = hit;
+        *out = std::move(hit);
+        return SV_OK;
+      }
+    }
   }
+  // miss: prepare and upload outside the lock into a fresh buffer, then publish
+  auto ent = std::make_shared<LineEntry>();
+  memcpy(ent->key, key, sizeof key);
+  ent->device = device;
   std::vector<LineCoeff> h(2 * ATE_NUM_LINES);
   g2_prepare(q1, h.data());
   g2_prepare(q2, h.data() + ATE_NUM_LINES);
-  if (!c.d_lines) SV_HIP(hipMalloc(&c.d_lines, h.size() * sizeof(LineCoeff)));
-  SV_HIP(hipMemcpyAsync(c.d_lines, h.data(), h.size() * sizeof(LineCoeff), hipMemcpyHostToDevice, st));
+  SV_HIP(hipMalloc(&ent->d_lines, h.size() * sizeof(LineCoeff)));
+  SV_HIP(hipMemcpyAsync(ent->d_lines, h.data(), h.size() * sizeof(LineCoeff), hipMemcpyHostToDevice, st));
   SV_HIP(hipStreamSynchronize(st));
-  memcpy(c.key, key, sizeof key);
-  c.valid = true;
-  *out = c.d_lines;
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    for (int j = kLineCacheKeys - 1; j > 0; j--) c.e[j] = c.e[j - 1];
+    c.e[0] = ent;
+  }
+  *out = std::move(ent);
   return SV_OK;
 }
 
@@ -638,8 +672,9 @@ int decide_run_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const vo
   if (!lease.ok()) return SV_ERR_DEVICE;
   Workspace* ws = lease.get();
   hipStream_t st = ws->stream;
-  const LineCoeff* lines = nullptr;
-  SV_TRY(decider_lines(g2, s_g2, form, device, st, &lines));
+  std::shared_ptr<LineEntry> line_ref;  // held until the stream has synchronised (below)
+  SV_TRY(decider_lines(g2, s_g2, form, device, st, &line_ref));
+  const LineCoeff* lines = line_ref->d_lines;
   size_t bytes = Workspace::aligned(n * 4) + (gt_host ? Workspace::aligned(n * sizeof(Fq12)) : 0);
   SV_TRY(ws->reserve(bytes));
   SV_TRY(ws->reserve_pinned(n * 4 + 256));

@@ -128,13 +128,17 @@ inline F f_inv(const F& a) {
   return r;
 }
 
-inline bool f_is_reduced(const F& a) {
+inline bool f_is_reduced(const F& a, const uint64_t (&mod)[4] = P64) {
   for (int i = 3; i >= 0; i--) {
-    if (a.l[i] < P64[i]) return true;
-    if (a.l[i] > P64[i]) return false;
+    if (a.l[i] < mod[i]) return true;
+    if (a.l[i] > mod[i]) return false;
   }
   return false;
 }
+
+// scalar-field order r (Fr), for validating host-side scalar inputs
+static constexpr uint64_t R64[4] = {0x43e1f593f0000001ull, 0x2833e84879b97091ull,
+                                    0xb85045b68181585dull, 0x30644e72e131a029ull};
 
 // XYZZ point (Montgomery), identity ZZ = 0.  Layout identical to device sv::G1Xyzz.
 struct Xyzz {

@@ -197,6 +197,10 @@ __global__ void __launch_bounds__(kThreads) k_msm_batch_windows(const G1Aff* __r
             }
             const uint32_t* bp = reinterpret_cast<const uint32_t*>(bases + bi);
             Fq x = ld_fq(bp), y = ld_fq(bp + 8);
+            if (!x.is_reduced() || !y.is_reduced()) {  // same contract as the single-MSM path
+              atomicOr(err, 1u);
+              continue;
+            }
             if (x.is_zero() && y.is_zero()) continue;  // identity base
             if (!mont_b) {
               x = fe_to_mont(x);
@@ -404,6 +408,10 @@ int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t*
   SV_HIP(hipStreamSynchronize(st));
   uint32_t ev;
   memcpy(&ev, ws->pinned, 4);
+  if (ev & 1u) {
+    set_error("msm_batch: base coordinate not reduced mod p");
+    return SV_ERR_ARG;
+  }
   if (ev & 2u) {
     set_error("msm_batch: scalar not reduced (>= r)");
     return SV_ERR_ARG;

@@ -154,3 +154,19 @@ def test_codec_arguments_rejected_without_compute():
     recs[0x180 + 64] = 1  # record 1 carries a different G2 than record 0
     assert _lib.lib.sv_bn254_kzg_decide_eip197(recs.ctypes.data, 2, 0, ctypes.byref(ff)) == _lib.SV_ERR_ARG
     assert "differ" in _lib.last_error()
+
+
+def test_accumulate_rejects_unreduced_r_without_compute():
+    """sv_bn254_kzg_accumulate validates r < the Fr order on the host, like every other scalar input."""
+    from svgpu import _lib
+    from svgpu import encoding as enc
+    pts = enc.bases_array([b.G1_GEN])
+    out_l, out_r = _lib.sv_g1_affine(), _lib.sv_g1_affine()
+    for bad in (b.R, b.R + 5, (1 << 256) - 1):
+        rr = _lib.sv_fe()
+        for i in range(4):
+            rr.l[i] = (bad >> (64 * i)) & ((1 << 64) - 1)
+        rc = _lib.lib.sv_bn254_kzg_accumulate(pts.ctypes.data, pts.ctypes.data, 1, ctypes.byref(rr), 0, 0,
+                                              ctypes.byref(out_l), ctypes.byref(out_r))
+        assert rc == _lib.SV_ERR_ARG, bad
+        assert "not reduced" in _lib.last_error()

@@ -165,3 +165,16 @@ def test_indexed_device_api_matches_direct(gpu, oracle_cpp):
     idx[5] = rows
     with pytest.raises(svgpu.ArgumentError):
         dv.msm_batch_indexed(T, idx, Sd, off, m)
+
+
+@pytest.mark.parametrize("seq_max", ["0", "1000"])
+def test_unreduced_base_rejected_on_both_routes(gpu, oracle_cpp, monkeypatch, seq_max):
+    """A base coordinate >= p is SV_ERR_ARG whichever route the batch takes (the batched kernel
+    and the sequential single-MSM route share the contract of k_to_mont_bases)."""
+    import svgpu
+    monkeypatch.setenv("SVGPU_BATCH_SEQ_MAX", seq_max)
+    B, S, off = _ragged(oracle_cpp, [8, 8, 8, 8, 8, 8], 321)
+    B = B.copy()
+    B[13, 0:4] = np.array([0xffffffffffffffff] * 4, np.uint64)  # x = 2^256 - 1 >= p
+    with pytest.raises(svgpu.ArgumentError):
+        svgpu.msm_batch_arrays(B, S, off)

@@ -66,9 +66,22 @@ const char* sv_version(void) SV_NOEXCEPT;
 /* ---- a1/a3: multi-scalar multiplication ---------------------------------------------
  * out = sum_i scalars[i] * bases[i] as an affine point (identity -> (0,0)).
  * Host buffers.  num_gpus <= 0 means every initialised device (point-sharded, partials
- * folded in device order).  Scalars must be reduced (< r) in the given form.              */
+ * folded in device order).  Scalars must be reduced (< r) in the given form.  The inputs
+ * reach HBM in pieces (SVGPU_H2D_PIECES, default 4) on a copy stream, each piece's sort and
+ * bucket accumulation overlapping the next piece's transfer; device buffers are pooled.   */
 int sv_bn254_g1_msm(const sv_g1_affine* bases, const sv_fe* scalars, size_t n, int form,
                     int num_gpus, sv_g1_affine* out) SV_NOEXCEPT;
+
+/* The same MSM over the exact shape NativeLoader::multi_scalar_multiplication receives
+ * (native.rs:61-71: pairs: &[(&Fr, &G1Affine)], an array of references into scattered
+ * caller memory).  The library gathers the referenced 96 B per pair on its host worker pool
+ * straight into pinned staging, piece by piece, and each piece's DMA and sort overlap the
+ * gather of the next -- the shim passes its pairs as this 16-B-per-pair struct array (a Rust
+ * tuple's field order is unspecified, so the shim maps (&Fr, &G1Affine) into sv_msm_ref).
+ * A NULL reference is SV_ERR_ARG.                                                          */
+typedef struct { const sv_fe* scalar; const sv_g1_affine* base; } sv_msm_ref;
+int sv_bn254_g1_msm_refs(const sv_msm_ref* pairs, size_t n, int form, int num_gpus,
+                         sv_g1_affine* out) SV_NOEXCEPT;
 
 /* Device-resident variant (bases/scalars already in HBM on `device`, `stream` may be NULL):
  * writes this shard's partial sum to *out_partial (host memory, Jacobian, canonical form).
@@ -212,6 +225,8 @@ typedef struct {
   uint64_t entries;
 } sv_msm_stats;
 int sv_msm_last_stats(sv_msm_stats* out) SV_NOEXCEPT;
+/* Kernel time (HIP events on the call's stream) of the calling thread's last decider launch. */
+int sv_kzg_last_kernel_ms(float* out) SV_NOEXCEPT;
 
 #ifdef __cplusplus
 }

@@ -86,7 +86,12 @@ inline F fsub(const Mod& m, const F& a, const F& b) {
   sub_in(r.l, b.l);
   return r;
 }
+// Fp-multiplication counter (the decider's algorithmic work is counted on this
+// restatement): off unless or_count_decide_fpmul runs, one relaxed flag test per product otherwise.
+static bool g_count_on = false;
+static thread_local uint64_t g_fq_muls = 0;
 inline F fmul(const Mod& m, const F& a, const F& b) {
+  if (g_count_on && &m == &FQ) g_fq_muls++;
   uint64_t t[6] = {0, 0, 0, 0, 0, 0};
   for (int i = 0; i < 4; i++) {
     u128 c = 0;
@@ -705,6 +710,20 @@ int or_decide_all(const uint64_t* g2, const uint64_t* s_g2, const uint64_t* lhs,
       break;
     }
   return 0;
+}
+
+// Fq multiplications (squarings included) of ONE decide (decider.rs:60-68) as restated here:
+// two G2 line preparations, the 2-pair Miller loop and the final exponentiation.
+uint64_t or_count_decide_fpmul(const uint64_t* g2, const uint64_t* s_g2, const uint64_t* lhs, const uint64_t* rhs) {
+  init_consts();
+  G2A q1 = load_g2(g2), q2 = load_g2(s_g2);
+  q2.y = f2n(q2.y);
+  const A l = load_aff(lhs), r = load_aff(rhs);
+  g_fq_muls = 0;
+  g_count_on = true;
+  (void)decide_gt(q1, q2, l, r);
+  g_count_on = false;
+  return g_fq_muls;
 }
 
 // KzgAs::create_proof without blind: lhs = sum r^i lhs_i, rhs = sum r^i rhs_i (naive MSMs, as

@@ -26,6 +26,8 @@ def lib():
         L.or_msm_pippenger.argtypes = [c_void_p, c_void_p, c_size_t, c_int, c_void_p]
         L.or_decide_all.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int,
                                     ctypes.POINTER(c_int32), c_void_p]
+        L.or_count_decide_fpmul.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p]
+        L.or_count_decide_fpmul.restype = c_uint64
         L.or_accumulate.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p]
         L.or_gen_scalars.argtypes = [c_uint64, c_uint64, c_size_t, c_void_p]
         L.or_gen_scalars.restype = None
@@ -67,6 +69,12 @@ def decide_all(g2: np.ndarray, s_g2: np.ndarray, lhs, rhs, threads: int = 1, wan
                            ctypes.byref(ff), gt.ctypes.data if gt is not None else None):
         raise AssertionError("assertion failed: !accumulators.is_empty()")
     return ff.value, gt
+
+
+def count_decide_fpmul(g2: np.ndarray, s_g2: np.ndarray, lhs_row, rhs_row) -> int:
+    """Fq multiplications of one decide as restated in bn254_ref.cpp (decider roofline)."""
+    g2, s_g2, l, r = _c(g2), _c(s_g2), _c(lhs_row), _c(rhs_row)
+    return int(lib().or_count_decide_fpmul(g2.ctypes.data, s_g2.ctypes.data, l.ctypes.data, r.ctypes.data))
 
 
 def accumulate(lhs, rhs, r: np.ndarray):

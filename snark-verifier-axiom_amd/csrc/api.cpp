@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -89,23 +90,50 @@ int for_each_device(int ndev, Fn fn) {
   return SV_OK;
 }
 
-// Owned device buffer on `device` (host-buffer API path).
-struct DevBuf {
-  void* p = nullptr;
-  int dev = 0;
-  ~DevBuf() {
-    if (p) {
-      hipSetDevice(dev);
-      hipFree(p);
+// Pooled device staging for the host-buffer entry points: the regions live in a leased
+// workspace's grow-only input buffer (no per-call hipMalloc / hipFree); copies run on the lease's
+// stream and are synchronised before the call returns.
+struct Staging {
+  WsLease lease;
+  std::vector<char*> d;
+  explicit Staging(int device) : lease(device, nullptr) {}
+  int init(std::initializer_list<size_t> sizes) {
+    if (!lease.ok()) return SV_ERR_DEVICE;
+    size_t tot = 0;
+    for (size_t s : sizes) tot += Workspace::aligned(s ? s : 1);
+    SV_TRY(lease.get()->reserve_in(tot));
+    char* p = lease.get()->inbuf;
+    for (size_t s : sizes) {
+      d.push_back(p);
+      p += Workspace::aligned(s ? s : 1);
     }
+    return SV_OK;
   }
-  int alloc(int device, size_t bytes) {
-    dev = device;
-    SV_HIP(hipSetDevice(device));
-    SV_HIP(hipMalloc(&p, bytes ? bytes : 1));
+  template <class T = void>
+  T* at(int i) const {
+    return reinterpret_cast<T*>(d[i]);
+  }
+  int put(int i, const void* h, size_t bytes) {
+    if (bytes) SV_HIP(hipMemcpyAsync(d[i], h, bytes, hipMemcpyHostToDevice, lease.get()->stream));
+    return SV_OK;
+  }
+  int get(void* h, int i, size_t bytes) {
+    if (bytes) SV_HIP(hipMemcpyAsync(h, d[i], bytes, hipMemcpyDeviceToHost, lease.get()->stream));
+    return SV_OK;
+  }
+  int sync() {
+    SV_HIP(hipStreamSynchronize(lease.get()->stream));
     return SV_OK;
   }
 };
+
+// pieces of a host-fed MSM (SVGPU_H2D_PIECES, default 4): piece k + 1's transfer overlaps piece
+// k's sort and accumulation
+int h2d_pieces() {
+  const char* e = getenv("SVGPU_H2D_PIECES");
+  const int p = e ? atoi(e) : 4;
+  return p < 1 ? 1 : p;
+}
 
 #define SV_GUARD_BEGIN try {
 #define SV_GUARD_END                                    \
@@ -167,13 +195,104 @@ int sv_bn254_g1_msm(const sv_g1_affine* bases, const sv_fe* scalars, size_t n, i
   int rc = for_each_device(ndev, [&](int k, int dev) -> int {
     size_t lo = k * per, hi = std::min(n, lo + per);
     if (lo >= hi) return SV_OK;
-    size_t m = hi - lo;
-    DevBuf db, ds;
-    SV_TRY(db.alloc(dev, m * sizeof(sv_g1_affine)));
-    SV_TRY(ds.alloc(dev, m * sizeof(sv_fe)));
-    SV_HIP(hipMemcpy(db.p, bases + lo, m * sizeof(sv_g1_affine), hipMemcpyHostToDevice));
-    SV_HIP(hipMemcpy(ds.p, scalars + lo, m * sizeof(sv_fe), hipMemcpyHostToDevice));
-    return msm_run_device(db.p, ds.p, m, form, dev, nullptr, &part[k]);
+    MsmFeed feed;
+    feed.pieces = h2d_pieces();
+    feed.stage = [&, lo](size_t a, size_t b, void* db, void* ds, hipStream_t cs, hipEvent_t sc_ready,
+                         hipEvent_t b_ready) -> int {
+      // pageable caller memory: the runtime's staged DMA measured at the pinned rate (tools/ubench_h2d.cpp)
+      SV_HIP(hipMemcpyAsync(ds, scalars + lo + a, (b - a) * sizeof(sv_fe), hipMemcpyHostToDevice, cs));
+      SV_HIP(hipEventRecord(sc_ready, cs));
+      SV_HIP(hipMemcpyAsync(db, bases + lo + a, (b - a) * sizeof(sv_g1_affine), hipMemcpyHostToDevice, cs));
+      SV_HIP(hipEventRecord(b_ready, cs));
+      return SV_OK;
+    };
+    return msm_run_fed(hi - lo, form, dev, feed, &part[k]);
+  });
+  if (rc != SV_OK) return rc;
+  Xyzz acc = host::x_identity();
+  for (auto& p : part) acc = host::x_add(acc, p);
+  affine_out(acc, form, out);
+  return SV_OK;
+  SV_GUARD_END
+}
+
+// references gathered this far ahead are prefetched (random 32/64-B reads are DRAM-latency bound)
+static constexpr size_t kGatherAhead = 16;
+
+int sv_bn254_g1_msm_refs(const sv_msm_ref* pairs, size_t n, int form, int num_gpus, sv_g1_affine* out) noexcept {
+  SV_GUARD_BEGIN
+  if (n == 0) {
+    sv::set_error("pairs should not be empty");
+    return SV_ERR_EMPTY;
+  }
+  if (!pairs || !out) {
+    sv::set_error("null pointer");
+    return SV_ERR_ARG;
+  }
+  SV_TRY(check_form(form));
+  int ndev = resolve_gpus(num_gpus);
+  if (ndev == 0) return SV_ERR_DEVICE;
+  if ((size_t)ndev > n) ndev = (int)n;
+  std::vector<Xyzz> part(ndev, host::x_identity());
+  size_t per = (n + ndev - 1) / ndev;
+  int rc = for_each_device(ndev, [&](int k, int dev) -> int {
+    size_t lo = k * per, hi = std::min(n, lo + per);
+    if (lo >= hi) return SV_OK;
+    const size_t m = hi - lo;
+    // the gather target: pinned staging of a leased workspace (grow-only, reused across calls)
+    WsLease st_lease(dev, nullptr);
+    if (!st_lease.ok()) return SV_ERR_DEVICE;
+    Workspace* sw = st_lease.get();
+    SV_TRY(sw->reserve_stage(m * (sizeof(sv_fe) + sizeof(sv_g1_affine))));
+    sv_fe* hs = reinterpret_cast<sv_fe*>(sw->stage);
+    sv_g1_affine* hb = reinterpret_cast<sv_g1_affine*>(sw->stage + m * sizeof(sv_fe));
+    std::atomic<int> null_ref{0};
+    MsmFeed feed;
+    feed.pieces = h2d_pieces();
+    feed.stage = [&, lo](size_t a, size_t b, void* db, void* ds, hipStream_t cs, hipEvent_t sc_ready,
+                         hipEvent_t b_ready) -> int {
+      // gather piece [a, b) on the host pool (scalars, then bases: the scalar DMA overlaps the
+      // base gather, and this piece's DMA the next piece's gather)
+      host_parallel_for(b - a, 8192, [&](size_t x, size_t y) {
+        for (size_t i = a + x; i < a + y; i++) {
+          if (i + kGatherAhead < a + y) __builtin_prefetch(pairs[lo + i + kGatherAhead].scalar);
+          const sv_fe* sp = pairs[lo + i].scalar;
+          if (!sp) {
+            null_ref.store(1);
+            memset(&hs[i], 0, sizeof(sv_fe));
+          } else {
+            hs[i] = *sp;
+          }
+        }
+      });
+      SV_HIP(hipMemcpyAsync(ds, hs + a, (b - a) * sizeof(sv_fe), hipMemcpyHostToDevice, cs));
+      SV_HIP(hipEventRecord(sc_ready, cs));
+      host_parallel_for(b - a, 8192, [&](size_t x, size_t y) {
+        for (size_t i = a + x; i < a + y; i++) {
+          if (i + kGatherAhead < a + y) {
+            const char* q = reinterpret_cast<const char*>(pairs[lo + i + kGatherAhead].base);
+            __builtin_prefetch(q);
+            __builtin_prefetch(q + 63);  // a 64-B point may straddle two lines
+          }
+          const sv_g1_affine* bp = pairs[lo + i].base;
+          if (!bp) {
+            null_ref.store(1);
+            memset(&hb[i], 0, sizeof(sv_g1_affine));
+          } else {
+            hb[i] = *bp;
+          }
+        }
+      });
+      SV_HIP(hipMemcpyAsync(db, hb + a, (b - a) * sizeof(sv_g1_affine), hipMemcpyHostToDevice, cs));
+      SV_HIP(hipEventRecord(b_ready, cs));
+      return SV_OK;
+    };
+    int r = msm_run_fed(m, form, dev, feed, &part[k]);
+    if (r == SV_OK && null_ref.load()) {
+      sv::set_error("null scalar or base reference");
+      return SV_ERR_ARG;
+    }
+    return r;
   });
   if (rc != SV_OK) return rc;
   Xyzz acc = host::x_identity();
@@ -249,13 +368,13 @@ int sv_bn254_kzg_decide(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const 
     size_t lo = k * per, hi = std::min(n, lo + per);
     if (lo >= hi) return SV_OK;
     size_t m = hi - lo;
-    DevBuf dl, dr;
-    SV_TRY(dl.alloc(dev, m * sizeof(sv_g1_affine)));
-    SV_TRY(dr.alloc(dev, m * sizeof(sv_g1_affine)));
-    SV_HIP(hipMemcpy(dl.p, lhs + lo, m * sizeof(sv_g1_affine), hipMemcpyHostToDevice));
-    SV_HIP(hipMemcpy(dr.p, rhs + lo, m * sizeof(sv_g1_affine), hipMemcpyHostToDevice));
+    Staging sg(dev);
+    SV_TRY(sg.init({m * sizeof(sv_g1_affine), m * sizeof(sv_g1_affine)}));
+    SV_TRY(sg.put(0, lhs + lo, m * sizeof(sv_g1_affine)));
+    SV_TRY(sg.put(1, rhs + lo, m * sizeof(sv_g1_affine)));
+    SV_TRY(sg.sync());
     int32_t f = -1;
-    SV_TRY(decide_run_device(g2, s_g2, dl.p, dr.p, m, form, dev, nullptr, &f, nullptr, nullptr));
+    SV_TRY(decide_run_device(g2, s_g2, sg.at(0), sg.at(1), m, form, dev, nullptr, &f, nullptr, nullptr));
     ff[k] = f < 0 ? -1 : (int32_t)(lo + f);
     return SV_OK;
   });
@@ -303,19 +422,17 @@ int sv_bn254_kzg_accumulate(const sv_g1_affine* lhs, const sv_g1_affine* rhs, si
   }
   if (resolve_gpus(1) == 0) return SV_ERR_DEVICE;
   int dev = runtime_device_id(0);
-  DevBuf dbl, dbr, dsc, drr;
-  SV_TRY(dbl.alloc(dev, n * sizeof(sv_g1_affine)));
-  SV_TRY(dbr.alloc(dev, n * sizeof(sv_g1_affine)));
-  SV_TRY(dsc.alloc(dev, n * sizeof(sv_fe)));
-  SV_TRY(drr.alloc(dev, sizeof(sv_fe)));
-  SV_HIP(hipMemcpy(dbl.p, lhs, n * sizeof(sv_g1_affine), hipMemcpyHostToDevice));
-  SV_HIP(hipMemcpy(dbr.p, rhs, n * sizeof(sv_g1_affine), hipMemcpyHostToDevice));
-  SV_HIP(hipMemcpy(drr.p, r, sizeof(sv_fe), hipMemcpyHostToDevice));
-  SV_TRY(powers_device(drr.p, form, n, form, dsc.p, nullptr));
-  SV_HIP(hipDeviceSynchronize());
+  Staging sg(dev);
+  SV_TRY(sg.init({n * sizeof(sv_g1_affine), n * sizeof(sv_g1_affine), n * sizeof(sv_fe), sizeof(sv_fe)}));
+  SV_TRY(sg.put(0, lhs, n * sizeof(sv_g1_affine)));
+  SV_TRY(sg.put(1, rhs, n * sizeof(sv_g1_affine)));
+  SV_TRY(sg.put(3, r, sizeof(sv_fe)));
+  SV_TRY(sg.sync());
+  SV_TRY(powers_device(sg.at(3), form, n, form, sg.at(2), sg.lease.get()->stream));
+  SV_TRY(sg.sync());
   Xyzz a, b;
-  SV_TRY(msm_run_device(dbl.p, dsc.p, n, form, dev, nullptr, &a));
-  SV_TRY(msm_run_device(dbr.p, dsc.p, n, form, dev, nullptr, &b));
+  SV_TRY(msm_run_device(sg.at(0), sg.at(2), n, form, dev, nullptr, &a));
+  SV_TRY(msm_run_device(sg.at(1), sg.at(2), n, form, dev, nullptr, &b));
   affine_out(a, form, out_lhs);
   affine_out(b, form, out_rhs);
   return SV_OK;
@@ -363,24 +480,23 @@ int sv_bn254_g1_msm_batch(const sv_g1_affine* bases, const sv_fe* scalars, const
       max_small = std::max(max_small, m);
     }
   }
-  DevBuf db, ds, doff, dids, dout;
-  SV_TRY(db.alloc(dev, total * sizeof(sv_g1_affine)));
-  SV_TRY(ds.alloc(dev, total * sizeof(sv_fe)));
-  SV_TRY(doff.alloc(dev, (count + 1) * sizeof(uint64_t)));
-  SV_TRY(dids.alloc(dev, count * sizeof(uint32_t)));
-  SV_TRY(dout.alloc(dev, count * sizeof(sv_g1_affine)));
-  SV_HIP(hipMemcpy(db.p, bases + base, total * sizeof(sv_g1_affine), hipMemcpyHostToDevice));
-  SV_HIP(hipMemcpy(ds.p, scalars + base, total * sizeof(sv_fe), hipMemcpyHostToDevice));
-  SV_HIP(hipMemcpy(doff.p, off.data(), (count + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
+  Staging sg(dev);
+  SV_TRY(sg.init({total * sizeof(sv_g1_affine), total * sizeof(sv_fe), (count + 1) * sizeof(uint64_t),
+                  count * sizeof(uint32_t), count * sizeof(sv_g1_affine)}));
+  SV_TRY(sg.put(0, bases + base, total * sizeof(sv_g1_affine)));
+  SV_TRY(sg.put(1, scalars + base, total * sizeof(sv_fe)));
+  SV_TRY(sg.put(2, off.data(), (count + 1) * sizeof(uint64_t)));
+  SV_TRY(sg.put(3, small_ids.data(), small_ids.size() * sizeof(uint32_t)));
+  SV_TRY(sg.sync());
   if (!small_ids.empty()) {
-    SV_HIP(hipMemcpy(dids.p, small_ids.data(), small_ids.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    SV_TRY(msm_batch_device(db.p, ds.p, static_cast<const uint64_t*>(doff.p), static_cast<const uint32_t*>(dids.p),
-                            small_ids.size(), max_small, form, dev, nullptr, dout.p));
-    SV_HIP(hipMemcpy(out, dout.p, count * sizeof(sv_g1_affine), hipMemcpyDeviceToHost));
+    SV_TRY(msm_batch_device(sg.at(0), sg.at(1), sg.at<const uint64_t>(2), sg.at<const uint32_t>(3),
+                            small_ids.size(), max_small, form, dev, nullptr, sg.at(4)));
+    SV_TRY(sg.get(out, 4, count * sizeof(sv_g1_affine)));
+    SV_TRY(sg.sync());
   }
   for (uint32_t k : big_ids) {
     Xyzz r;
-    SV_TRY(msm_run_device(static_cast<const sv_g1_affine*>(db.p) + off[k], static_cast<const sv_fe*>(ds.p) + off[k],
+    SV_TRY(msm_run_device(sg.at<const sv_g1_affine>(0) + off[k], sg.at<const sv_fe>(1) + off[k],
                           off[k + 1] - off[k], form, dev, nullptr, &r));
     affine_out(r, form, &out[k]);
   }
@@ -530,17 +646,17 @@ int sv_bn254_g1_msm_batch_table(uint64_t handle, const uint32_t* base_idx, const
                     (unsigned long long)(base + i), t.n);
       return SV_ERR_ARG;
     }
-  DevBuf didx, ds, doff, dout;
-  SV_TRY(didx.alloc(t.dev, total * sizeof(uint32_t)));
-  SV_TRY(ds.alloc(t.dev, total * sizeof(sv_fe)));
-  SV_TRY(doff.alloc(t.dev, (count + 1) * sizeof(uint64_t)));
-  SV_TRY(dout.alloc(t.dev, count * sizeof(sv_g1_affine)));
-  SV_HIP(hipMemcpy(didx.p, base_idx + base, total * sizeof(uint32_t), hipMemcpyHostToDevice));
-  SV_HIP(hipMemcpy(ds.p, scalars + base, total * sizeof(sv_fe), hipMemcpyHostToDevice));
-  SV_HIP(hipMemcpy(doff.p, off.data(), (count + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
-  SV_TRY(msm_batch_device(t.p, ds.p, static_cast<const uint64_t*>(doff.p), nullptr, count, max_terms, form, t.dev,
-                          nullptr, dout.p, static_cast<const uint32_t*>(didx.p), t.n, SV_MONTGOMERY));
-  SV_HIP(hipMemcpy(out, dout.p, count * sizeof(sv_g1_affine), hipMemcpyDeviceToHost));
+  Staging sg(t.dev);
+  SV_TRY(sg.init({total * sizeof(uint32_t), total * sizeof(sv_fe), (count + 1) * sizeof(uint64_t),
+                  count * sizeof(sv_g1_affine)}));
+  SV_TRY(sg.put(0, base_idx + base, total * sizeof(uint32_t)));
+  SV_TRY(sg.put(1, scalars + base, total * sizeof(sv_fe)));
+  SV_TRY(sg.put(2, off.data(), (count + 1) * sizeof(uint64_t)));
+  SV_TRY(sg.sync());
+  SV_TRY(msm_batch_device(t.p, sg.at(1), sg.at<const uint64_t>(2), nullptr, count, max_terms, form, t.dev, nullptr,
+                          sg.at(3), sg.at<const uint32_t>(0), t.n, SV_MONTGOMERY));
+  SV_TRY(sg.get(out, 3, count * sizeof(sv_g1_affine)));
+  SV_TRY(sg.sync());
   return SV_OK;
   SV_GUARD_END
 }
@@ -577,11 +693,12 @@ int sv_bn254_poseidon_permute(sv_fe* states, size_t n, int t, int form) noexcept
   if (resolve_gpus(1) == 0) return SV_ERR_DEVICE;
   const int dev = runtime_device_id(0);
   const size_t bytes = n * (size_t)t * sizeof(sv_fe);
-  DevBuf d;
-  SV_TRY(d.alloc(dev, bytes));
-  SV_HIP(hipMemcpy(d.p, states, bytes, hipMemcpyHostToDevice));
-  SV_TRY(poseidon_permute_device(d.p, n, t, form, nullptr));
-  SV_HIP(hipMemcpy(states, d.p, bytes, hipMemcpyDeviceToHost));
+  Staging sg(dev);
+  SV_TRY(sg.init({bytes}));
+  SV_TRY(sg.put(0, states, bytes));
+  SV_TRY(poseidon_permute_device(sg.at(0), n, t, form, sg.lease.get()->stream));
+  SV_TRY(sg.get(states, 0, bytes));
+  SV_TRY(sg.sync());
   return SV_OK;
   SV_GUARD_END
 }
@@ -618,17 +735,16 @@ int sv_bn254_poseidon_squeeze(sv_fe* states, const sv_fe* elements, const uint64
   std::vector<uint64_t> off(offsets, offsets + n + 1);
   for (auto& o : off) o -= offsets[0];
   const size_t sbytes = n * (size_t)t * sizeof(sv_fe);
-  DevBuf ds, de, doff, dout;
-  SV_TRY(ds.alloc(dev, sbytes));
-  SV_TRY(de.alloc(dev, total * sizeof(sv_fe)));
-  SV_TRY(doff.alloc(dev, (n + 1) * sizeof(uint64_t)));
-  SV_TRY(dout.alloc(dev, n * sizeof(sv_fe)));
-  SV_HIP(hipMemcpy(ds.p, states, sbytes, hipMemcpyHostToDevice));
-  if (total) SV_HIP(hipMemcpy(de.p, elements + offsets[0], total * sizeof(sv_fe), hipMemcpyHostToDevice));
-  SV_HIP(hipMemcpy(doff.p, off.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
-  SV_TRY(poseidon_squeeze_device(ds.p, de.p, static_cast<const uint64_t*>(doff.p), n, t, form, dout.p, nullptr));
-  SV_HIP(hipMemcpy(states, ds.p, sbytes, hipMemcpyDeviceToHost));
-  if (out) SV_HIP(hipMemcpy(out, dout.p, n * sizeof(sv_fe), hipMemcpyDeviceToHost));
+  Staging sg(dev);
+  SV_TRY(sg.init({sbytes, total * sizeof(sv_fe), (n + 1) * sizeof(uint64_t), n * sizeof(sv_fe)}));
+  SV_TRY(sg.put(0, states, sbytes));
+  if (total) SV_TRY(sg.put(1, elements + offsets[0], total * sizeof(sv_fe)));
+  SV_TRY(sg.put(2, off.data(), (n + 1) * sizeof(uint64_t)));
+  SV_TRY(poseidon_squeeze_device(sg.at(0), sg.at(1), sg.at<const uint64_t>(2), n, t, form, sg.at(3),
+                                 sg.lease.get()->stream));
+  SV_TRY(sg.get(states, 0, sbytes));
+  if (out) SV_TRY(sg.get(out, 3, n * sizeof(sv_fe)));
+  SV_TRY(sg.sync());
   return SV_OK;
   SV_GUARD_END
 }
@@ -658,12 +774,13 @@ int sv_bn254_g1_decode(const uint8_t* data, size_t n, int encoding, int form, sv
   if (resolve_gpus(1) == 0) return SV_ERR_DEVICE;
   const int dev = runtime_device_id(0);
   const size_t rec = encoding == SV_ENC_EVM ? 64 : 32;
-  DevBuf din, dout;
-  SV_TRY(din.alloc(dev, n * rec));
-  SV_TRY(dout.alloc(dev, n * sizeof(sv_g1_affine)));
-  SV_HIP(hipMemcpy(din.p, data, n * rec, hipMemcpyHostToDevice));
-  SV_TRY(g1_decode_device(din.p, n, encoding, rec, 0, form, dev, nullptr, dout.p, &fi));
-  SV_HIP(hipMemcpy(out, dout.p, n * sizeof(sv_g1_affine), hipMemcpyDeviceToHost));
+  Staging sg(dev);
+  SV_TRY(sg.init({n * rec, n * sizeof(sv_g1_affine)}));
+  SV_TRY(sg.put(0, data, n * rec));
+  SV_TRY(sg.sync());
+  SV_TRY(g1_decode_device(sg.at(0), n, encoding, rec, 0, form, dev, nullptr, sg.at(1), &fi));
+  SV_TRY(sg.get(out, 1, n * sizeof(sv_g1_affine)));
+  SV_TRY(sg.sync());
   if (first_invalid) *first_invalid = fi;
   if (fi >= 0) {
     sv::set_error("Invalid elliptic curve point encoding in proof (point %lld)", (long long)fi);
@@ -701,15 +818,15 @@ int sv_bn254_kzg_accumulators_from_limbs(const sv_fe* limbs, size_t n, int n_lim
   if (resolve_gpus(1) == 0) return SV_ERR_DEVICE;
   const int dev = runtime_device_id(0);
   const size_t nl = n * 4 * (size_t)n_limbs;
-  DevBuf dl, dlhs, drhs;
-  SV_TRY(dl.alloc(dev, nl * sizeof(sv_fe)));
-  SV_TRY(dlhs.alloc(dev, n * sizeof(sv_g1_affine)));
-  SV_TRY(drhs.alloc(dev, n * sizeof(sv_g1_affine)));
-  SV_HIP(hipMemcpy(dl.p, limbs, nl * sizeof(sv_fe), hipMemcpyHostToDevice));
+  Staging sg(dev);
+  SV_TRY(sg.init({nl * sizeof(sv_fe), n * sizeof(sv_g1_affine), n * sizeof(sv_g1_affine)}));
+  SV_TRY(sg.put(0, limbs, nl * sizeof(sv_fe)));
+  SV_TRY(sg.sync());
   int64_t fi = -1;
-  SV_TRY(limbs_to_accumulators_device(dl.p, n, n_limbs, bits, form, dev, nullptr, dlhs.p, drhs.p, &fi));
-  SV_HIP(hipMemcpy(lhs, dlhs.p, n * sizeof(sv_g1_affine), hipMemcpyDeviceToHost));
-  SV_HIP(hipMemcpy(rhs, drhs.p, n * sizeof(sv_g1_affine), hipMemcpyDeviceToHost));
+  SV_TRY(limbs_to_accumulators_device(sg.at(0), n, n_limbs, bits, form, dev, nullptr, sg.at(1), sg.at(2), &fi));
+  SV_TRY(sg.get(lhs, 1, n * sizeof(sv_g1_affine)));
+  SV_TRY(sg.get(rhs, 2, n * sizeof(sv_g1_affine)));
+  SV_TRY(sg.sync());
   if (first_invalid) *first_invalid = fi;
   if (fi >= 0) {
     sv::set_error("accumulator %lld: limbs do not encode a canonical on-curve point", (long long)fi);
@@ -769,16 +886,16 @@ int sv_bn254_kzg_decide_eip197(const uint8_t* input, size_t n_checks, int num_gp
   }
   if (resolve_gpus(1) == 0) return SV_ERR_DEVICE;
   const int dev = runtime_device_id(0);
-  DevBuf din, dl, dr;
-  SV_TRY(din.alloc(dev, n_checks * kRec));
-  SV_TRY(dl.alloc(dev, n_checks * sizeof(sv_g1_affine)));
-  SV_TRY(dr.alloc(dev, n_checks * sizeof(sv_g1_affine)));
-  SV_HIP(hipMemcpy(din.p, input, n_checks * kRec, hipMemcpyHostToDevice));
+  Staging sg(dev);
+  SV_TRY(sg.init({n_checks * kRec, n_checks * sizeof(sv_g1_affine), n_checks * sizeof(sv_g1_affine)}));
+  SV_TRY(sg.put(0, input, n_checks * kRec));
+  SV_TRY(sg.sync());
   int64_t bl = -1, br = -1;
-  SV_TRY(g1_decode_device(din.p, n_checks, SV_ENC_EVM, kRec, 0, SV_CANONICAL, dev, nullptr, dl.p, &bl));
-  SV_TRY(g1_decode_device(din.p, n_checks, SV_ENC_EVM, kRec, 192, SV_CANONICAL, dev, nullptr, dr.p, &br));
+  SV_TRY(g1_decode_device(sg.at(0), n_checks, SV_ENC_EVM, kRec, 0, SV_CANONICAL, dev, nullptr, sg.at(1), &bl));
+  SV_TRY(g1_decode_device(sg.at(0), n_checks, SV_ENC_EVM, kRec, 192, SV_CANONICAL, dev, nullptr, sg.at(2), &br));
   int32_t ff = -1;
-  SV_TRY(decide_run_device(&g2, &sg2, dl.p, dr.p, n_checks, SV_CANONICAL, dev, nullptr, &ff, nullptr, nullptr));
+  SV_TRY(decide_run_device(&g2, &sg2, sg.at(1), sg.at(2), n_checks, SV_CANONICAL, dev, nullptr, &ff, nullptr,
+                           nullptr));
   int64_t first = -1;
   for (int64_t c : {(int64_t)ff, bl, br})
     if (c >= 0 && (first < 0 || c < first)) first = c;
@@ -810,6 +927,12 @@ int sv_msm_last_stats(sv_msm_stats* out) noexcept {
   if (!out) return SV_ERR_ARG;
   return msm_last_stats(out);
   SV_GUARD_END
+}
+
+int sv_kzg_last_kernel_ms(float* out) noexcept {
+  if (!out) return SV_ERR_ARG;
+  *out = decider_last_kernel_ms();
+  return SV_OK;
 }
 
 }  // extern "C"

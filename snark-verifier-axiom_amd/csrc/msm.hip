@@ -664,6 +664,22 @@ __global__ void __launch_bounds__(kBlock) k_fixup_heavy(const uint32_t* __restri
   }
 }
 
+// Host-fed pieces: bucket sums of piece k >= 1 (emptiness from its gst) added into piece 0's.  The
+// first merge also reads piece 0's emptiness (gst_acc) and writes every bucket, so afterwards bsum
+// holds all W * B buckets (identity where empty) and k_wsum runs without an emptiness table.
+__global__ void __launch_bounds__(kBlock) k_merge_buckets(G1Xyzz* __restrict__ acc, const uint32_t* __restrict__ gst_acc,
+                                                          const G1Xyzz* __restrict__ x, const uint32_t* __restrict__ gst_x,
+                                                          uint32_t nbt) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nbt) return;
+  const bool ea = gst_acc && gst_acc[b] == gst_acc[b + 1];
+  const bool ex = gst_x[b] == gst_x[b + 1];
+  if (ex && !ea) return;  // nothing to add, acc already written
+  G1Xyzz a = ea ? G1Xyzz::identity() : load_xyzz(acc, b);
+  if (!ex) a = xyzz_add(a, load_xyzz(x, b));
+  store_xyzz(acc, b, a);
+}
+
 // One bucket-reduction level over `groups` groups of N elements, segments of L buckets:
 //   acc[g][j] = sum_{i in seg j} (i - jL + base) X[g][i],  tot[g][j] = sum_{i in seg j} X[g][i]
 // Empty buckets (gst[b] == gst[b + 1]) are never written by the accumulate pass and read as identity.
@@ -674,7 +690,7 @@ __global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, c
   if (tid >= J * groups) return;
   uint32_t g = tid / J, j = tid % J;
   const G1Xyzz* x = X + (size_t)g * N;
-  const uint32_t* gs = gst + (size_t)g * N;
+  const uint32_t* gs = gst ? gst + (size_t)g * N : nullptr;  // null: every bucket written
   uint32_t lo = j * L;
   uint32_t hi = min(N, lo + L);
   G1Xyzz run = G1Xyzz::identity(), acc = G1Xyzz::identity();
@@ -682,7 +698,7 @@ __global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, c
     // bucket i - 1 (and its emptiness) is loaded while bucket i is being added (A/B at 2^20:
     // reduce 0.404 -> 0.393 ms)
     uint32_t i = hi - 1;
-    uint32_t gn = gs[i + 1], g0 = gs[i];
+    uint32_t gn = gs ? gs[i + 1] : 1u, g0 = gs ? gs[i] : 0u;
     bool ne = g0 != gn;
     G1Xyzz nx = ne ? load_xyzz(x, i) : G1Xyzz::identity();
     for (;;) {
@@ -692,7 +708,7 @@ __global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, c
       if (ci > lo) {
         i = ci - 1;
         gn = g0;
-        g0 = gs[i];
+        g0 = gs ? gs[i] : gn + 1u;
         ne = g0 != gn;
         if (ne) nx = load_xyzz(x, i);
       }
@@ -856,8 +872,66 @@ static host::Xyzz host_combine(const MsmPlan& p, const host::Xyzz* A /* [W][NG] 
   return acc;
 }
 
-int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int form, int device,
-                   hipStream_t user_stream, host::Xyzz* out) {
+// One piece's front half: digits + two-level sort + bucket accumulation + crossing-bucket fixups
+// of points [0, m) of (bases, scalars) into bsum (complete buckets only; emptiness from gst).
+struct MsmScratch {
+  uint32_t *err, *bcnt, *btot, *bstart, *gst, *ent, *tstart, *heavy, *multi, *nheavy, *nmulti;
+  uint64_t* tmp;
+  G1Xyzz *pfirst, *plast;
+};
+
+static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, const void* dsrc, size_t m,
+                     int mont_in, int device, hipStream_t st, G1Xyzz* bsum, const G1Aff* phi, uint32_t nsplit,
+                     hipEvent_t ev_sorted, hipEvent_t ev_sort_mid, hipEvent_t ev_acc_done, hipEvent_t ev_fix_mid,
+                     hipEvent_t bases_ready, const G1Aff* conv_src) {
+  const int LOGB = p.c - 1;
+  const int nb = p.glv ? 128 : 255;
+  const uint32_t CB = (uint32_t)coarse_bits(p.c, nb), FB = (uint32_t)LOGB - CB, NBIN = 1u << CB;
+  const uint32_t nwb = p.W * NBIN;
+  const uint32_t npts = (uint32_t)m;
+  const uint32_t nblk = cdiv(npts, sort_chunk(p.c, nb));
+  const uint32_t T = cdiv((uint64_t)npts * p.W, p.K);
+  SV_LAUNCH_C(k_bin_hist, p.glv, p.c, dim3(nblk), dim3(kBlock), dsrc, npts, mont_in, nblk, w.bcnt, w.err);
+  SV_HIP(hipGetLastError());
+  if (ev_sort_mid) SV_HIP(hipEventRecord(ev_sort_mid, st));
+  hipLaunchKernelGGL(k_bin_scan_chunks, dim3(nwb), dim3(kBlock), 0, st, w.bcnt, nblk, w.btot);
+  hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, w.btot, nwb, w.bstart);
+  SV_LAUNCH_C(k_bin_scatter, p.glv, p.c, dim3(nblk), dim3(kBlock), dsrc, npts, mont_in, nblk, w.bcnt, w.bstart,
+              w.tmp);
+  static thread_local int fine_attr_dev = -1;  // the > 64 KiB dynamic-LDS opt-in, once per thread/device
+  if (fine_attr_dev != device) {
+    SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort<false>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFineLds));
+    SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort<true>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFineLds));
+    fine_attr_dev = device;
+  }
+  hipLaunchKernelGGL(k_fine_sort<false>, dim3(nwb), dim3(1024), kFineLds, st, w.tmp, w.bstart, FB, p.K, w.gst,
+                     w.tstart, w.ent);
+  hipLaunchKernelGGL(k_fine_sort<true>, dim3(nwb), dim3(1024), kFineLds, st, w.tmp, w.bstart, FB, p.K, w.gst,
+                     w.tstart, w.ent);
+  SV_HIP(hipMemcpyAsync(w.gst + p.nbt, w.bstart + nwb, 4, hipMemcpyDeviceToDevice, st));
+  SV_HIP(hipGetLastError());
+  if (bases_ready) SV_HIP(hipStreamWaitEvent(st, bases_ready, 0));
+  if (conv_src)  // host-fed canonical bases: converted once they have landed, after the sort
+    hipLaunchKernelGGL(k_to_mont_bases, dim3(cdiv(npts, kBlock)), dim3(kBlock), 0, st, conv_src,
+                       const_cast<G1Aff*>(bases), npts, w.err);
+  if (ev_sorted) SV_HIP(hipEventRecord(ev_sorted, st));
+  hipLaunchKernelGGL(k_accumulate, dim3(cdiv(T, kBlock)), dim3(kBlock), 0, st, bases, w.ent, w.gst, w.tstart,
+                     p.nbt, p.K, T, bsum, w.pfirst, w.plast, w.multi, w.nmulti, phi, nsplit);
+  SV_HIP(hipGetLastError());
+  if (ev_acc_done) SV_HIP(hipEventRecord(ev_acc_done, st));
+  hipLaunchKernelGGL(k_fixup_multi, dim3(std::min<uint32_t>(cdiv(p.nbt, kBlock), 1024)), dim3(kBlock), 0, st,
+                     w.gst, p.K, w.pfirst, w.plast, w.multi, w.nmulti, bsum, w.heavy, w.nheavy);
+  hipLaunchKernelGGL(k_fixup_heavy, dim3(256), dim3(kBlock), 0, st, w.gst, p.K, w.pfirst, w.plast, w.heavy,
+                     w.nheavy, bsum);
+  SV_HIP(hipGetLastError());
+  if (ev_fix_mid) SV_HIP(hipEventRecord(ev_fix_mid, st));
+  return SV_OK;
+}
+
+static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, int form, int device,
+                        hipStream_t user_stream, const MsmFeed* feed, host::Xyzz* out) {
   if (n == 0) {
     set_error("pairs should not be empty");
     return SV_ERR_EMPTY;
@@ -874,39 +948,58 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
   if (!lease.ok()) return SV_ERR_DEVICE;
   Workspace* ws = lease.get();
   hipStream_t st = ws->stream;
-  const MsmPlan p = msm_plan(n);
-  const uint64_t entries = (uint64_t)p.npts * p.W;
+  MsmPlan p = msm_plan(n);
+  // host-fed inputs arrive in pieces: piece k's sort + accumulate run while piece k + 1 is in flight
+  int pieces = 1;
+  if (feed) {
+    pieces = feed->pieces < 1 ? 1 : feed->pieces;
+    if (p.glv || n < (size_t)pieces * 4096) pieces = 1;
+    if (pieces > 8) pieces = 8;
+  }
+  const size_t max_piece = (n + pieces - 1) / pieces;
+  const uint64_t entries = (uint64_t)(p.glv ? 2 * n : max_piece) * p.W;  // per piece
+  const uint32_t Tmax = cdiv(entries, p.K);
 
-  // ---- workspace layout
+  // ---- workspace layout (sort / accumulate scratch sized for the largest piece)
   const int LOGB = p.c - 1;
-  // (128 coarse bins for 2^21 full-width points, LDS-staged regions, measured no faster: the scatter
-  // runs and the per-block count table grow as much as the fine sort saves)
-  const uint32_t CB = (uint32_t)coarse_bits(p.c, p.glv ? 128 : 255), FB = (uint32_t)LOGB - CB, NBIN = 1u << CB;
+  const int nb = p.glv ? 128 : 255;
+  const uint32_t CB = (uint32_t)coarse_bits(p.c, nb), NBIN = 1u << CB;
+  (void)LOGB;
   const uint32_t nwb = p.W * NBIN;
-  const uint32_t nblk = cdiv(p.npts, sort_chunk(p.c, p.glv ? 128 : 255));
+  const uint32_t nblk = cdiv(p.glv ? 2 * n : max_piece, sort_chunk(p.c, nb));
   size_t bytes = 0;
   auto add = [&](size_t b) { bytes += Workspace::aligned(b); };
-  bool conv = (form == SV_CANONICAL);
+  const bool conv = (form == SV_CANONICAL);
   if (conv) add(n * sizeof(G1Aff));
   if (p.glv) add(2 * n * sizeof(uint4));      // GLV scalar halves
   if (p.glv) add(n * sizeof(G1Aff));          // phi(P)
-  add(256);                                   // err flag + heavy-queue counter
+  add(256);                                   // err flag + heavy/multi queue counters
   add((size_t)nwb * nblk * 4);                // bcnt
   add((size_t)nwb * 4);                       // btot
   add(((size_t)nwb + 1) * 4);                 // bstart
   add(entries * 8);                           // tmp (coarse-binned entries)
   add(((size_t)p.nbt + 1) * 4);               // gst
   add(entries * 4);                           // ent
-  add(((size_t)p.T + 1) * 4);                 // tstart
-  add((size_t)p.T * sizeof(G1Xyzz) * 2);      // pfirst, plast
+  add(((size_t)Tmax + 1) * 4);                // tstart
+  add((size_t)Tmax * sizeof(G1Xyzz) * 2);     // pfirst, plast
   add((size_t)p.nbt * sizeof(G1Xyzz));        // bsum
   add((size_t)p.nbt * 4);                     // heavy-bucket queue
   add((size_t)p.nbt * 4);                     // multi-thread-bucket queue
+  if (pieces > 1) {
+    add((size_t)p.nbt * sizeof(G1Xyzz));      // bsum of pieces 1..
+    add(((size_t)p.nbt + 1) * 4);             // gst of piece 0
+  }
   const size_t nfinal = (size_t)p.W * p.NG;
   add((size_t)p.J * p.W * sizeof(G1Xyzz) * 2);  // acc_j, T_j
   add(nfinal * sizeof(G1Xyzz));                 // group sums
   SV_TRY(ws->reserve(bytes));
   SV_TRY(ws->reserve_pinned(nfinal * sizeof(G1Xyzz) + 256));
+  if (feed) {
+    SV_TRY(ws->reserve_in(Workspace::aligned(n * sizeof(G1Aff)) + Workspace::aligned(n * sizeof(Fr))));
+    SV_TRY(ws->ensure_copy_stream());
+    d_bases = ws->inbuf;
+    d_scalars = ws->inbuf + Workspace::aligned(n * sizeof(G1Aff));
+  }
 
   const G1Aff* bases = reinterpret_cast<const G1Aff*>(d_bases);
   const Fr* scalars = reinterpret_cast<const Fr*>(d_scalars);
@@ -914,81 +1007,95 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
   G1Aff* bases_m = conv ? ws->carve<G1Aff>(n) : nullptr;
   uint4* hs = p.glv ? ws->carve<uint4>(2 * n) : nullptr;
   G1Aff* phi = p.glv ? ws->carve<G1Aff>(n) : nullptr;
-  uint32_t* err = ws->carve<uint32_t>(64);
-  uint32_t* bcnt = ws->carve<uint32_t>((size_t)nwb * nblk);
-  uint32_t* btot = ws->carve<uint32_t>(nwb);
-  uint32_t* bstart = ws->carve<uint32_t>((size_t)nwb + 1);
-  uint64_t* tmp = ws->carve<uint64_t>(entries);
-  uint32_t* gst = ws->carve<uint32_t>((size_t)p.nbt + 1);
-  uint32_t* ent = ws->carve<uint32_t>(entries);
-  uint32_t* tstart = ws->carve<uint32_t>((size_t)p.T + 1);
-  G1Xyzz* pfirst = ws->carve<G1Xyzz>(p.T);
-  G1Xyzz* plast = ws->carve<G1Xyzz>(p.T);
+  MsmScratch w;
+  w.err = ws->carve<uint32_t>(64);
+  w.bcnt = ws->carve<uint32_t>((size_t)nwb * nblk);
+  w.btot = ws->carve<uint32_t>(nwb);
+  w.bstart = ws->carve<uint32_t>((size_t)nwb + 1);
+  w.tmp = ws->carve<uint64_t>(entries);
+  w.gst = ws->carve<uint32_t>((size_t)p.nbt + 1);
+  w.ent = ws->carve<uint32_t>(entries);
+  w.tstart = ws->carve<uint32_t>((size_t)Tmax + 1);
+  w.pfirst = ws->carve<G1Xyzz>(Tmax);
+  w.plast = ws->carve<G1Xyzz>(Tmax);
   G1Xyzz* bsum = ws->carve<G1Xyzz>(p.nbt);
-  uint32_t* heavy = ws->carve<uint32_t>(p.nbt);
-  uint32_t* multi = ws->carve<uint32_t>(p.nbt);
-  uint32_t* nheavy = err + 1;  // zeroed with the error flag
-  uint32_t* nmulti = err + 2;
+  w.heavy = ws->carve<uint32_t>(p.nbt);
+  w.multi = ws->carve<uint32_t>(p.nbt);
+  w.nheavy = w.err + 1;  // zeroed with the error flag
+  w.nmulti = w.err + 2;
+  G1Xyzz* bsum_k = pieces > 1 ? ws->carve<G1Xyzz>(p.nbt) : nullptr;
+  uint32_t* gst0 = pieces > 1 ? ws->carve<uint32_t>((size_t)p.nbt + 1) : nullptr;
   G1Xyzz* racc = ws->carve<G1Xyzz>((size_t)p.J * p.W);
   G1Xyzz* rtot = ws->carve<G1Xyzz>((size_t)p.J * p.W);
   G1Xyzz* ping = ws->carve<G1Xyzz>(nfinal);
 
   hipEvent_t* ev = ws->ev;
-  SV_HIP(hipEventRecord(ev[0], st));
-  SV_HIP(hipMemsetAsync(err, 0, 256, st));
-  if (conv) {
-    hipLaunchKernelGGL(k_to_mont_bases, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, st,
-                       bases, bases_m, (uint32_t)n, err);
-    bases = bases_m;
-  }
-  const void* dsrc = scalars;  // what the sort passes take digits from
-  if (p.glv) {
-    hipLaunchKernelGGL(k_glv_prep, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, st, bases, scalars, (uint32_t)n, mont_in,
-                       hs, phi, err);
-    dsrc = hs;
-  }
-  const uint32_t npts = (uint32_t)p.npts;
-  SV_LAUNCH_C(k_bin_hist, p.glv, p.c, dim3(nblk), dim3(kBlock), dsrc, npts, mont_in, nblk, bcnt, err);
-  SV_HIP(hipGetLastError());
   // each event record between kernels costs ~5.5 us of idle GPU (rocprof trace): the accumulate is
   // always bracketed (bench.py's live roofline), the sort / fixup splits only with SVGPU_MSM_STATS=1
   static const bool detail = getenv("SVGPU_MSM_STATS") && atoi(getenv("SVGPU_MSM_STATS")) != 0;
-  if (detail) SV_HIP(hipEventRecord(ev[1], st));
-  hipLaunchKernelGGL(k_bin_scan_chunks, dim3(nwb), dim3(kBlock), 0, st, bcnt, nblk, btot);
-  hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, btot, nwb, bstart);
-  SV_LAUNCH_C(k_bin_scatter, p.glv, p.c, dim3(nblk), dim3(kBlock), dsrc, npts, mont_in, nblk, bcnt, bstart,
-              tmp);
-  static thread_local int fine_attr_dev = -1;  // the > 64 KiB dynamic-LDS opt-in, once per thread/device
-  if (fine_attr_dev != device) {
-    SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort<false>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFineLds));
-    SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort<true>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFineLds));
-    fine_attr_dev = device;
+  SV_HIP(hipEventRecord(ev[0], st));
+  SV_HIP(hipMemsetAsync(w.err, 0, 256, st));
+  if (feed && p.glv) {  // the GLV split needs every base and scalar first: one piece, then the device path
+    SV_HIP(hipEventRecord(ev[6], st));
+    SV_HIP(hipStreamWaitEvent(ws->copy_stream, ev[6], 0));
+    SV_TRY(feed->stage(0, n, const_cast<void*>(d_bases), const_cast<void*>(d_scalars), ws->copy_stream, ws->ev[8],
+                       ws->ev[9]));
+    SV_HIP(hipStreamWaitEvent(st, ws->ev[8], 0));
+    SV_HIP(hipStreamWaitEvent(st, ws->ev[9], 0));
   }
-  hipLaunchKernelGGL(k_fine_sort<false>, dim3(nwb), dim3(1024), kFineLds, st, tmp, bstart, FB, p.K, gst, tstart, ent);
-  hipLaunchKernelGGL(k_fine_sort<true>, dim3(nwb), dim3(1024), kFineLds, st, tmp, bstart, FB, p.K, gst, tstart, ent);
-  SV_HIP(hipMemcpyAsync(gst + p.nbt, bstart + nwb, 4, hipMemcpyDeviceToDevice, st));
-  SV_HIP(hipGetLastError());
-  SV_HIP(hipEventRecord(ev[2], st));
-  hipLaunchKernelGGL(k_accumulate, dim3(cdiv(p.T, kBlock)), dim3(kBlock), 0, st, bases, ent, gst,
-                     tstart, p.nbt, p.K, p.T, bsum, pfirst, plast, multi, nmulti, phi,
-                     p.glv ? (uint32_t)n : ~0u);
-  SV_HIP(hipGetLastError());
-  SV_HIP(hipEventRecord(ev[3], st));
-  hipLaunchKernelGGL(k_fixup_multi, dim3(std::min<uint32_t>(cdiv(p.nbt, kBlock), 1024)), dim3(kBlock), 0, st,
-                     gst, p.K, pfirst, plast, multi, nmulti, bsum, heavy, nheavy);
-  hipLaunchKernelGGL(k_fixup_heavy, dim3(256), dim3(kBlock), 0, st, gst, p.K, pfirst, plast, heavy, nheavy,
-                     bsum);
-  if (detail) SV_HIP(hipEventRecord(ev[4], st));
-  // bucket reduction: running sums over segments of 2^logL buckets, then the subset sums
-  hipLaunchKernelGGL(k_wsum, dim3(cdiv((uint64_t)p.J * p.W, kBlock)), dim3(kBlock), 0, st, bsum, gst, p.B, p.J,
-                     1u << p.logL, p.W, 1, racc, rtot);
+  if (!feed || p.glv) {
+    if (conv) {
+      hipLaunchKernelGGL(k_to_mont_bases, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, st, bases, bases_m, (uint32_t)n,
+                         w.err);
+      bases = bases_m;
+    }
+    const void* dsrc = scalars;  // what the sort passes take digits from
+    if (p.glv) {
+      hipLaunchKernelGGL(k_glv_prep, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, st, bases, scalars, (uint32_t)n,
+                         mont_in, hs, phi, w.err);
+      dsrc = hs;
+    }
+    SV_TRY(msm_front(p, w, bases, dsrc, p.npts, mont_in, device, st, bsum, phi, p.glv ? (uint32_t)n : ~0u, ev[2],
+                     detail ? ev[1] : nullptr, ev[3], detail ? ev[4] : nullptr, nullptr, nullptr));
+  } else {
+    // Piece k: the copy stream stages its scalars, then its bases; the compute stream sorts the
+    // piece once its scalars have landed and accumulates it once its bases have (k_to_mont_bases
+    // first for canonical input).  Pieces >= 1 are merged into piece 0's bucket sums.
+    hipStream_t cs = ws->copy_stream;
+    SV_HIP(hipEventRecord(ev[6], st));
+    SV_HIP(hipStreamWaitEvent(cs, ev[6], 0));  // the previous call's readers of inbuf are done
+    for (int k = 0; k < pieces; k++) {
+      const size_t lo = n * k / pieces, hi = n * (k + 1) / pieces, m = hi - lo;
+      hipEvent_t sc_ready = ws->ev[8 + 2 * k], b_ready = ws->ev[9 + 2 * k];
+      G1Aff* db = const_cast<G1Aff*>(reinterpret_cast<const G1Aff*>(d_bases)) + lo;
+      Fr* dsc = const_cast<Fr*>(scalars) + lo;
+      SV_TRY(feed->stage(lo, hi, db, dsc, cs, sc_ready, b_ready));
+      SV_HIP(hipStreamWaitEvent(st, sc_ready, 0));
+      if (k > 0) SV_HIP(hipMemsetAsync(w.err + 1, 0, 8, st));  // fixup queue counters
+      const G1Aff* pb = conv ? bases_m + lo : db;
+      G1Xyzz* dst = k == 0 ? bsum : bsum_k;
+      SV_TRY(msm_front(p, w, pb, dsc, m, mont_in, device, st, dst, nullptr, ~0u, k == 0 ? ev[2] : nullptr, nullptr,
+                       k == pieces - 1 ? ev[3] : nullptr, nullptr, b_ready, conv ? db : nullptr));
+      if (pieces > 1) {
+        if (k == 0) {
+          SV_HIP(hipMemcpyAsync(gst0, w.gst, ((size_t)p.nbt + 1) * 4, hipMemcpyDeviceToDevice, st));
+        } else {
+          hipLaunchKernelGGL(k_merge_buckets, dim3(cdiv(p.nbt, kBlock)), dim3(kBlock), 0, st, bsum,
+                             k == 1 ? gst0 : nullptr, bsum_k, w.gst, p.nbt);
+          SV_HIP(hipGetLastError());
+        }
+      }
+    }
+  }
+  // bucket reduction: running sums over segments of 2^logL buckets, then the subset sums (after a
+  // piece merge every bucket of bsum is written: no emptiness table)
+  hipLaunchKernelGGL(k_wsum, dim3(cdiv((uint64_t)p.J * p.W, kBlock)), dim3(kBlock), 0, st, bsum,
+                     pieces > 1 ? nullptr : w.gst, p.B, p.J, 1u << p.logL, p.W, 1, racc, rtot);
   hipLaunchKernelGGL(k_group_sum, dim3(p.NG * p.W), dim3(kGroupBlock), 0, st, racc, rtot, p.J, p.logJ, ping);
   SV_HIP(hipGetLastError());
   SV_HIP(hipEventRecord(ev[5], st));
   SV_HIP(hipMemcpyAsync(ws->pinned, ping, nfinal * sizeof(G1Xyzz), hipMemcpyDeviceToHost, st));
-  SV_HIP(hipMemcpyAsync(ws->pinned + nfinal * sizeof(G1Xyzz), err, 4, hipMemcpyDeviceToHost, st));
+  SV_HIP(hipMemcpyAsync(ws->pinned + nfinal * sizeof(G1Xyzz), w.err, 4, hipMemcpyDeviceToHost, st));
   SV_HIP(hipStreamSynchronize(st));
   uint32_t errv;
   memcpy(&errv, ws->pinned + nfinal * sizeof(G1Xyzz), 4);
@@ -1002,34 +1109,44 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
   auto t1 = std::chrono::steady_clock::now();
 
   sv_msm_stats& s = g_last_stats;
-  float ms;
-  if (detail) {
-    hipEventElapsedTime(&ms, ev[0], ev[1]);
+  float ms = 0;
+  if (detail && !feed) {
+    (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
     s.digits_ms = ms;  // digits + coarse histogram (digits are recomputed, never stored)
-    hipEventElapsedTime(&ms, ev[1], ev[2]);
+    (void)hipEventElapsedTime(&ms, ev[1], ev[2]);
     s.sort_ms = ms;
-    hipEventElapsedTime(&ms, ev[3], ev[4]);
+    (void)hipEventElapsedTime(&ms, ev[3], ev[4]);
     s.fixup_ms = ms;
-    hipEventElapsedTime(&ms, ev[4], ev[5]);
+    (void)hipEventElapsedTime(&ms, ev[4], ev[5]);
     s.reduce_ms = ms;
   } else {  // digits folded into sort_ms, fixup into reduce_ms
     s.digits_ms = 0;
-    hipEventElapsedTime(&ms, ev[0], ev[2]);
+    (void)hipEventElapsedTime(&ms, ev[0], ev[2]);
     s.sort_ms = ms;
     s.fixup_ms = 0;
-    hipEventElapsedTime(&ms, ev[3], ev[5]);
+    (void)hipEventElapsedTime(&ms, ev[3], ev[5]);
     s.reduce_ms = ms;
   }
-  hipEventElapsedTime(&ms, ev[2], ev[3]);
+  // host-fed: "accumulate" spans the first piece's accumulate to the last piece's (transfers included)
+  (void)hipEventElapsedTime(&ms, ev[2], ev[3]);
   s.accumulate_ms = ms;
-  hipEventElapsedTime(&ms, ev[0], ev[5]);
+  (void)hipEventElapsedTime(&ms, ev[0], ev[5]);
   s.host_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
   s.total_ms = ms + s.host_ms;
   s.window_bits = p.c;
   s.num_windows = p.W;
-  s.accumulate_launch_units = p.T;
-  s.entries = entries;
+  s.accumulate_launch_units = cdiv((uint64_t)p.npts * p.W, p.K);
+  s.entries = (uint64_t)p.npts * p.W;
   return SV_OK;
+}
+
+int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int form, int device,
+                   hipStream_t user_stream, host::Xyzz* out) {
+  return msm_run_impl(d_bases, d_scalars, n, form, device, user_stream, nullptr, out);
+}
+
+int msm_run_fed(size_t n, int form, int device, const MsmFeed& feed, host::Xyzz* out) {
+  return msm_run_impl(nullptr, nullptr, n, form, device, nullptr, &feed, out);
 }
 
 }  // namespace sv

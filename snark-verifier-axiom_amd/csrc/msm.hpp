@@ -4,6 +4,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 
 #include "../../include/svgpu.h"
 #include "host_ec.hpp"
@@ -30,6 +31,18 @@ MsmPlan msm_plan(size_t n);
 // Device-resident MSM on `device`; result (XYZZ, Montgomery) on the host.
 int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int form, int device,
                    hipStream_t stream, host::Xyzz* out);
+
+// Host-fed MSM (the host-buffer entry points): the caller's inputs reach HBM in `pieces` pieces on
+// the workspace's copy stream.  stage(lo, hi, d_bases, d_scalars, copy_stream, scalars_ready,
+// bases_ready) issues the transfers of points [lo, hi) into the given device pointers and records
+// the two events (scalars first: the piece's sort starts as soon as they land).
+struct MsmFeed {
+  int pieces = 4;
+  std::function<int(size_t lo, size_t hi, void* d_bases, void* d_scalars, hipStream_t copy_stream,
+                    hipEvent_t scalars_ready, hipEvent_t bases_ready)>
+      stage;
+};
+int msm_run_fed(size_t n, int form, int device, const MsmFeed& feed, host::Xyzz* out);
 
 int msm_last_stats(sv_msm_stats* out);
 

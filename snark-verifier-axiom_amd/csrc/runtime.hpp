@@ -6,6 +6,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -26,6 +27,13 @@ struct Workspace {
   size_t used = 0;
   char* pinned = nullptr;  // host staging
   size_t pinned_cap = 0;
+  // host-buffer entry points: pooled device copy of the caller's inputs (no per-call hipMalloc /
+  // hipFree), pinned gather staging, and a copy stream that runs ahead of `stream`
+  char* inbuf = nullptr;
+  size_t in_cap = 0;
+  char* stage = nullptr;
+  size_t stage_cap = 0;
+  hipStream_t copy_stream = nullptr;
   static constexpr int kEvents = 24;
   hipEvent_t ev[kEvents] = {};
 
@@ -41,7 +49,15 @@ struct Workspace {
   static size_t aligned(size_t bytes) { return (bytes + 255) & ~size_t(255); }
   int reserve(size_t bytes);         // grow-only; resets `used`
   int reserve_pinned(size_t bytes);  // grow-only pinned host staging
+  int reserve_in(size_t bytes);      // grow-only device input buffer
+  int reserve_stage(size_t bytes);   // grow-only pinned gather staging
+  int ensure_copy_stream();
 };
+
+// Host worker pool shared by every call (SVGPU_HOST_THREADS, default min(16, cores)): fn(lo, hi)
+// over contiguous slices of [0, n) of at least `grain` items, run on the pool and the caller.
+void host_parallel_for(size_t n, size_t grain, const std::function<void(size_t, size_t)>& fn);
+int host_threads();
 
 // RAII lease of a per-device workspace; stream override optional.
 class WsLease {

@@ -11,7 +11,7 @@ from ._lib import (SV_CANONICAL, SV_MONTGOMERY, ArgumentError, DeviceError, Empt
                    OutOfMemoryError, SvError, lib)
 from .kzg import AssertionFailure, KzgAccumulator, KzgAs, KzgDecidingKey
 from .loader import (BaseTable, NativeLoader, ReferencePanic, batch_multi_scalar_multiplication, fold_partials, msm_arrays,
-                     msm_batch_arrays, multi_scalar_multiplication)
+                     make_refs, msm_batch_arrays, msm_refs, multi_scalar_multiplication)
 
 
 def init(num_devices: int = 0) -> int:

@@ -89,6 +89,7 @@ PROTOTYPES = [
     ("sv_last_error", c_char_p, []),
     ("sv_version", c_char_p, []),
     ("sv_bn254_g1_msm", c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, POINTER(sv_g1_affine)]),
+    ("sv_bn254_g1_msm_refs", c_int, [c_void_p, c_size_t, c_int, c_int, POINTER(sv_g1_affine)]),
     ("sv_bn254_g1_msm_device", c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p, POINTER(sv_g1_jacobian)]),
     ("sv_bn254_g1_fold", c_int, [c_void_p, c_size_t, POINTER(sv_g1_affine), c_int]),
     ("sv_bn254_kzg_decide", c_int, [POINTER(sv_g2_affine), POINTER(sv_g2_affine), c_void_p, c_void_p, c_size_t,
@@ -119,6 +120,7 @@ PROTOTYPES = [
     ("sv_gen_scalars_device", c_int, [c_void_p, c_size_t, c_uint64, c_uint64, c_int, c_int, c_void_p]),
     ("sv_gen_bases_device", c_int, [c_void_p, c_size_t, c_uint64, c_uint64, c_int, c_int, c_void_p]),
     ("sv_msm_last_stats", c_int, [POINTER(sv_msm_stats)]),
+    ("sv_kzg_last_kernel_ms", c_int, [POINTER(c_float)]),
 ]
 
 

@@ -86,6 +86,13 @@ def decide(g2, s_g2, lhs: torch.Tensor, rhs: torch.Tensor, form: int = _lib.SV_C
     return ff.value, list(verdicts), gts
 
 
+def last_decide_kernel_ms() -> float:
+    """Kernel time of this thread's last decider launch (HIP events on the call's stream)."""
+    v = ctypes.c_float(0)
+    _lib.check(_lib.lib.sv_kzg_last_kernel_ms(ctypes.byref(v)), "sv_kzg_last_kernel_ms")
+    return float(v.value)
+
+
 def poseidon_squeeze(states: torch.Tensor, elements: torch.Tensor, offsets: torch.Tensor, t: int = 3,
                      form: int = _lib.SV_MONTGOMERY, out: torch.Tensor = None) -> torch.Tensor:
     """Poseidon::squeeze on n HBM-resident sponges (states: (n * t, 4) int64 limbs, in/out;

@@ -45,6 +45,28 @@ def msm_arrays(bases: np.ndarray, scalars: np.ndarray, form: int = _lib.SV_CANON
     return enc.g1_from_struct(out, form)
 
 
+def make_refs(scalar_ptrs: np.ndarray, base_ptrs: np.ndarray) -> np.ndarray:
+    """Pack two equal-length arrays of host addresses (scalar_ptrs[i] -> sv_fe, base_ptrs[i] ->
+    sv_g1_affine) into the (n, 2) u64 sv_msm_ref array of the C ABI."""
+    sp = np.ascontiguousarray(scalar_ptrs, dtype=np.uint64)
+    bp = np.ascontiguousarray(base_ptrs, dtype=np.uint64)
+    if sp.shape != bp.shape:
+        raise ReferencePanic("assertion failed: scalars.len() == bases.len()")
+    return np.stack([sp, bp], axis=1)
+
+
+def msm_refs(refs: np.ndarray, form: int = _lib.SV_CANONICAL, num_gpus: int = 0) -> Point:
+    """MSM over references (the NativeLoader pairs shape, native.rs:61-71): `refs` is the (n, 2)
+    u64 sv_msm_ref array (see make_refs); the library gathers the referenced values."""
+    refs = np.ascontiguousarray(refs, dtype=np.uint64).reshape(-1, 2)
+    out = _lib.sv_g1_affine()
+    rc = _lib.lib.sv_bn254_g1_msm_refs(refs.ctypes.data, refs.shape[0], form, num_gpus, ctypes.byref(out))
+    if rc == _lib.SV_ERR_EMPTY:
+        raise ReferencePanic("pairs should not be empty")
+    _lib.check(rc, "sv_bn254_g1_msm_refs")
+    return enc.g1_from_struct(out, form)
+
+
 def multi_scalar_multiplication(scalars: Sequence[int], bases: Sequence[Point], num_gpus: int = 0) -> Point:
     if len(scalars) != len(bases):
         raise ReferencePanic("assertion failed: scalars.len() == bases.len()")

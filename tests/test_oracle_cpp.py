@@ -2,7 +2,9 @@
 import numpy as np
 import pytest
 
-from conftest import pt, q2
+import os
+
+from conftest import ROOT, pt, q2
 from oracle import bn254 as b
 
 
@@ -65,3 +67,17 @@ def test_accumulate_golden(oracle_cpp, golden_decider):
 def test_empty_inputs_panic(oracle_cpp):
     with pytest.raises(AssertionError, match="pairs should not be empty"):
         oracle_cpp.msm_naive(np.zeros((0, 8), np.uint64), np.zeros((0, 4), np.uint64))
+
+
+def test_decide_fpmul_count_is_the_bench_constant():
+    """bench.py's FPMUL_RESTATEMENT is the instrumented restatement's Fq-product count per decide."""
+    import re
+    from oracle import cpu_ref
+    from svgpu import encoding as enc
+    g2, sg2, accs = b.gen_decider_case(2)
+    L = enc.bases_array([a[0] for a in accs])
+    R = enc.bases_array([a[1] for a in accs])
+    cnt = cpu_ref.count_decide_fpmul(np.frombuffer(b.g2_bytes(g2), np.uint64), np.frombuffer(b.g2_bytes(sg2), np.uint64),
+                                     L[0], R[0])
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert int(re.search(r"FPMUL_RESTATEMENT = (\d+)", src).group(1)) == cnt

@@ -11,7 +11,8 @@ from ctypes import c_int, c_int32, c_size_t, c_uint64, c_void_p
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "liboracle_bn254.so")
+LIB_PATH = os.environ.get("ORACLE_LIB",
+                          os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "liboracle_bn254.so"))
 _lib = None
 
 

@@ -1,0 +1,52 @@
+"""The Rust FFI crate (snark-verifier-gpu/src/lib.rs, uncompiled here: no Rust toolchain) declares
+every C-ABI function of include/svgpu.h with the same number of parameters, and its #[repr(C)]
+structs carry the header's fields in order -- so the binding a maintainer builds matches the
+library these tests exercise through ctypes."""
+import os
+import re
+
+from conftest import ROOT
+
+
+def _c_prototypes():
+    src = open(os.path.join(ROOT, "include", "svgpu.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    out = {}
+    for m in re.finditer(r"\bint\s+(sv_[a-z0-9_]+)\s*\(([^)]*)\)\s*SV_NOEXCEPT", src):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    for m in re.finditer(r"const char\*\s+(sv_[a-z0-9_]+)\s*\(void\)", src):
+        out[m.group(1)] = 0
+    return out
+
+
+def _rust_externs():
+    src = open(os.path.join(ROOT, "snark-verifier-gpu", "src", "lib.rs")).read()
+    block = src[src.index('extern "C" {'):]
+    block = block[:block.index("\n}\n")]
+    out = {}
+    for m in re.finditer(r"pub fn (sv_[a-z0-9_]+)\(([^)]*)\)", block, flags=re.S):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if not args else args.count(",") + 1 - (1 if args.endswith(",") else 0)
+    return out
+
+
+def test_rust_extern_block_matches_header():
+    c, r = _c_prototypes(), _rust_externs()
+    assert len(c) >= 28
+    assert set(c) == set(r), (set(c) ^ set(r))
+    for name, n in c.items():
+        assert r[name] == n, f"{name}: header has {n} params, Rust {r[name]}"
+
+
+def test_rust_structs_match_header_fields():
+    h = open(os.path.join(ROOT, "include", "svgpu.h")).read()
+    rs = open(os.path.join(ROOT, "snark-verifier-gpu", "src", "lib.rs")).read()
+    assert "typedef struct { const sv_fe* scalar; const sv_g1_affine* base; } sv_msm_ref;" in h
+    assert re.search(r"pub struct SvMsmRef \{\s*pub scalar: \*const SvFe,\s*pub base: \*const SvG1Affine,", rs)
+    assert re.search(r"pub struct SvG1Affine \{\s*pub x: SvFe,\s*pub y: SvFe,", rs)
+    assert re.search(r"pub struct SvFq2 \{\s*pub c0: SvFe,\s*pub c1: SvFe,", rs)
+    fields = re.search(r"typedef struct \{([^{}]*)\} sv_msm_stats;", h, flags=re.S).group(1)
+    names = re.findall(r"([a-z_]+)[,;]", fields)
+    rnames = re.findall(r"pub ([a-z_]+): (?:f32|u32|u64)", rs[rs.index("pub struct SvMsmStats"):])
+    assert names == rnames

@@ -105,6 +105,130 @@ def permutation(state: List[int], t: int, r_f: int, r_p: int, modulus: int = FR_
     return st
 
 
+# ---- the reference's optimised schedule (OptimizedPoseidonSpec, poseidon.rs:170-328) ---------------
+def _mat_mul(a, b, m):
+    n = len(a)
+    return [[sum(a[i][k] * b[k][j] for k in range(n)) % m for j in range(n)] for i in range(n)]
+
+
+def _transpose(a):
+    return [list(r) for r in zip(*a)]
+
+
+def _mul_vector(mat, v, m):  # MDSMatrix::mul_vector, poseidon.rs:101-109
+    return [sum(mat[i][j] * v[j] for j in range(len(v))) % m for i in range(len(mat))]
+
+
+def _determinant(mat, m):  # MDSMatrix::determinant, poseidon.rs:139-165 (Gaussian elimination)
+    a = [list(r) for r in mat]
+    n = len(a)
+    res = 1
+    for i in range(n):
+        piv = i
+        while a[piv][i] % m == 0:
+            piv += 1
+            assert piv < n, "matrix is not invertible"
+        if piv != i:
+            res = -res
+            a[piv], a[i] = a[i], a[piv]
+        res = res * a[i][i] % m
+        inv = pow(a[i][i], m - 2, m)
+        for j in range(i + 1, n):
+            f = a[j][i] * inv % m
+            for k in range(i + 1, n):
+                a[j][k] = (a[j][k] - a[i][k] * f) % m
+    return res % m
+
+
+def _factorise(mat, m):
+    """MDSMatrix::factorise (poseidon.rs:167-226): M = M' M'' with M'' sparse ((row, col_hat))."""
+    t = len(mat)
+    rate = t - 1
+    w = [mat[i][0] for i in range(1, t)]
+    m_hat = [[mat[i + 1][j + 1] for j in range(rate)] for i in range(rate)]
+    det_inv = pow(_determinant(m_hat, m), m - 2, m)
+    w_hat = []
+    for j in range(rate):  # Cramer's rule: w_hat = m_hat^-1 w
+        mj = [list(r) for r in m_hat]
+        for i in range(rate):
+            mj[i][j] = w[i]
+        w_hat.append(_determinant(mj, m) * det_inv % m)
+    m_prime = [[1 if i == j else 0 for j in range(t)] for i in range(t)]
+    for i in range(rate):
+        for j in range(rate):
+            m_prime[i + 1][j + 1] = m_hat[i][j]
+    m_pp = [[1 if i == j else 0 for j in range(t)] for i in range(t)]
+    m_pp[0] = list(mat[0])
+    for i in range(rate):
+        m_pp[i + 1][0] = w_hat[i]
+    row = [m_pp[i][0] for i in range(t)]
+    col_hat = m_pp[0][1:]
+    return m_prime, (row, col_hat)
+
+
+@functools.lru_cache(maxsize=None)
+def optimized_spec(t: int, r_f: int, r_p: int, modulus: int = FR_MODULUS):
+    """OptimizedPoseidonSpec::new (poseidon.rs:230-245): constants (start, partial, end), the dense MDS,
+    pre_sparse_mds and the r_p sparse matrices (row, col_hat), from the same Grain constants as spec()."""
+    m = modulus
+    rc, mds = spec(t, r_f, r_p, m)
+    consts = [rc[r * t:(r + 1) * t] for r in range(r_f + r_p)]
+    # the inverse MDS (Poseidon128Pow5Gen returns it alongside; Gauss-Jordan here)
+    aug = [list(mds[i]) + [1 if i == j else 0 for j in range(t)] for i in range(t)]
+    for c in range(t):
+        piv = next(r for r in range(c, t) if aug[r][c] % m)
+        aug[c], aug[piv] = aug[piv], aug[c]
+        inv = pow(aug[c][c], m - 2, m)
+        aug[c] = [x * inv % m for x in aug[c]]
+        for r in range(t):
+            if r != c and aug[r][c]:
+                f = aug[r][c]
+                aug[r] = [(x - f * y) % m for x, y in zip(aug[r], aug[c])]
+    mds_inv = [row[t:] for row in aug]
+    half = r_f // 2
+    # calculate_optimized_constants, poseidon.rs:247-295
+    start = [list(consts[0])] + [_mul_vector(mds_inv, consts[r], m) for r in range(1, half)]
+    acc = list(consts[half + r_p])
+    partial = [0] * r_p
+    for k, c in zip(range(r_p - 1, -1, -1), [consts[r] for r in range(half + r_p - 1, half - 1, -1)]):
+        tmp = _mul_vector(mds_inv, acc, m)
+        partial[k] = tmp[0]
+        tmp[0] = 0
+        acc = [(x + y) % m for x, y in zip(tmp, c)]
+    start.append(_mul_vector(mds_inv, acc, m))
+    end = [_mul_vector(mds_inv, consts[r], m) for r in range(half + r_p + 1, r_f + r_p)]
+    # calculate_sparse_matrices, poseidon.rs:297-313
+    mds_t = _transpose(mds)
+    accm = [list(r) for r in mds_t]
+    sparse = []
+    for _ in range(r_p):
+        m_prime, mpp = _factorise(accm, m)
+        accm = _mat_mul(mds_t, m_prime, m)
+        sparse.append(mpp)
+    sparse.reverse()
+    pre_sparse = _transpose(accm)
+    return {"start": start, "partial": partial, "end": end, "mds": mds, "pre_sparse": pre_sparse, "sparse": sparse}
+
+
+def permutation_optimized(state: List[int], t: int, r_f: int, r_p: int, modulus: int = FR_MODULUS) -> List[int]:
+    """Poseidon::permutation (poseidon.rs:469-500) without the absorbed inputs and padding: the bare
+    HADES map in the reference's optimised schedule; equals permutation() (tests check it)."""
+    m = modulus
+    sp = optimized_spec(t, r_f, r_p, m)
+    st = [(x + c) % m for x, c in zip(state, sp["start"][0])]        # absorb_with_pre_constants
+    sbox = lambda v, c: (pow(v, 5, m) + c) % m  # noqa: E731  power5_with_constant
+    for cs in sp["start"][1:r_f // 2]:
+        st = _mul_vector(sp["mds"], [sbox(v, c) for v, c in zip(st, cs)], m)
+    st = _mul_vector(sp["pre_sparse"], [sbox(v, c) for v, c in zip(st, sp["start"][-1])], m)
+    for c, (row, col_hat) in zip(sp["partial"], sp["sparse"]):       # sbox_part + apply_sparse_mds
+        st[0] = sbox(st[0], c)
+        s0 = sum(r * v for r, v in zip(row, st)) % m
+        st = [s0] + [(ch * st[0] + v) % m for ch, v in zip(col_hat, st[1:])]
+    for cs in sp["end"]:
+        st = _mul_vector(sp["mds"], [sbox(v, c) for v, c in zip(st, cs)], m)
+    return _mul_vector(sp["mds"], [sbox(v, 0) for v in st], m)
+
+
 # widths the reference instantiates: t -> (R_F, R_P)  (tests.rs:39-42, :63-66; sdk halo2.rs:52-55)
 PARAMS = {3: (8, 57), 5: (8, 60)}
 

@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_scan_chunks(uint32_t* __restrict
 
 // one 1024-thread block: exclusive scan of btot over all (window, bin) -> bstart; bstart[nwb] = total
 __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __restrict__ btot, uint32_t nwb,
-                                                   uint32_t* __restrict__ bstart) {
+                                                   uint32_t* __restrict__ bstart, uint32_t* __restrict__ gst_end) {
   __shared__ uint32_t part[1024];
   const uint32_t tid = threadIdx.x;
   const uint32_t per = (nwb + 1023) / 1024;
@@ -307,7 +307,10 @@ __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __restrict__ 
     bstart[k] = run;
     run += btot[k];
   }
-  if (tid == 1023) bstart[nwb] = part[1023];
+  if (tid == 1023) {
+    bstart[nwb] = part[1023];
+    *gst_end = part[1023];  // gst[nbt]: the entry total (k_fine_sort writes the other bucket starts)
+  }
 }
 
 // Pass 3: the block's entries are first placed in LDS grouped by (window, bin), then each group
@@ -515,6 +518,7 @@ __global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__
 // occupancy, no global round trip).  Every other crossing bucket keeps the global pieces
 // (pfirst = a thread's first segment, plast = its last) and is queued for k_fixup_multi.  Empty
 // buckets are never written: k_wsum reads gst.
+static constexpr uint32_t kFixSerial = 8;  // crossing buckets of more pieces go to k_fixup_heavy
 __device__ __forceinline__ bool join_in_block(uint32_t gs, uint32_t ge, uint32_t K) {
   const uint32_t t0 = gs / K, t1 = (ge - 1) / K;
   return t1 == t0 + 1 && t0 / kBlock == t1 / kBlock;
@@ -523,8 +527,8 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
     const G1Aff* __restrict__ bases, const uint32_t* __restrict__ ent, const uint32_t* __restrict__ gst,
     const uint32_t* __restrict__ tstart, uint32_t nbt, uint32_t K, uint32_t T,
     G1Xyzz* __restrict__ bsum, G1Xyzz* __restrict__ pfirst, G1Xyzz* __restrict__ plast,
-    uint32_t* __restrict__ multi, uint32_t* __restrict__ nmulti, const G1Aff* __restrict__ phi,
-    uint32_t nsplit) {
+    uint32_t* __restrict__ multi, uint32_t* __restrict__ nmulti, uint32_t* __restrict__ heavy,
+    uint32_t* __restrict__ nheavy, const G1Aff* __restrict__ phi, uint32_t nsplit) {
   __shared__ G1Xyzz shead[kBlock];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t m = gst[nbt];
@@ -597,7 +601,8 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
       owner = true;
     } else {
       store_xyzz(first ? pfirst : plast, t, acc);
-      multi[atomicAdd(nmulti, 1u)] = g;
+      multi[atomicAdd(nmulti, 1u)] = g;  // joined by k_wsum (device path) or k_fixup_multi (host-fed)
+      if ((ge - 1) / K - gs / K > kFixSerial) heavy[atomicAdd(nheavy, 1u)] = g;
     }
   }
   __syncthreads();
@@ -606,8 +611,7 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
 
 // Queued crossing buckets (see k_accumulate): pieces pfirst/plast joined serially when the bucket
 // spans at most kFixSerial + 1 threads; longer ones (skewed digits: all-equal scalars, a short top
-// window) go on to k_fixup_heavy instead of being walked serially.
-static constexpr uint32_t kFixSerial = 8;
+// window) are queued by k_accumulate for k_fixup_heavy instead of being walked serially.
 __device__ __forceinline__ G1Xyzz fixup_head(const G1Xyzz* __restrict__ pfirst, const G1Xyzz* __restrict__ plast,
                                              uint32_t s, uint32_t t0, uint32_t K) {
   return (s == t0 * K) ? load_xyzz(pfirst, t0) : load_xyzz(plast, t0);
@@ -625,10 +629,7 @@ __global__ void __launch_bounds__(kBlock) k_fixup_multi(const uint32_t* __restri
     const uint32_t g = multi[h];
     const uint32_t s = gst[g], e = gst[g + 1];
     const uint32_t t0 = s / K, t1 = (e - 1) / K;
-    if (t1 - t0 > kFixSerial) {
-      heavy[atomicAdd(nheavy, 1u)] = g;
-      continue;
-    }
+    if (t1 - t0 > kFixSerial) continue;  // queued for k_fixup_heavy by k_accumulate
     G1Xyzz acc = fixup_head(pfirst, plast, s, t0, K);
     for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, load_xyzz(pfirst, t));
     store_xyzz(bsum, g, acc);
@@ -680,6 +681,17 @@ __global__ void __launch_bounds__(kBlock) k_merge_buckets(G1Xyzz* __restrict__ a
   store_xyzz(acc, b, a);
 }
 
+// Bucket i of one window (x, gs: that window's bucket sums and starts): false when empty.
+// gs == null: every bucket was written (host-fed merge).  (Joining the crossing buckets here
+// instead of in k_fixup_multi was measured 155 -> 440 us for k_wsum at 2^20: ~7 % of buckets cross,
+// so nearly every wave's iteration diverges into the join loop.)
+__device__ __forceinline__ bool bucket_at(const G1Xyzz* __restrict__ x, const uint32_t* __restrict__ gs, uint32_t i,
+                                          G1Xyzz& out) {
+  if (gs && gs[i] == gs[i + 1]) return false;
+  out = load_xyzz(x, i);
+  return true;
+}
+
 // One bucket-reduction level over `groups` groups of N elements, segments of L buckets:
 //   acc[g][j] = sum_{i in seg j} (i - jL + base) X[g][i],  tot[g][j] = sum_{i in seg j} X[g][i]
 // Empty buckets (gst[b] == gst[b + 1]) are never written by the accumulate pass and read as identity.
@@ -690,7 +702,7 @@ __global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, c
   if (tid >= J * groups) return;
   uint32_t g = tid / J, j = tid % J;
   const G1Xyzz* x = X + (size_t)g * N;
-  const uint32_t* gs = gst ? gst + (size_t)g * N : nullptr;  // null: every bucket written
+  const uint32_t* gs = gst ? gst + (size_t)g * N : nullptr;
   uint32_t lo = j * L;
   uint32_t hi = min(N, lo + L);
   G1Xyzz run = G1Xyzz::identity(), acc = G1Xyzz::identity();
@@ -698,19 +710,15 @@ __global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, c
     // bucket i - 1 (and its emptiness) is loaded while bucket i is being added (A/B at 2^20:
     // reduce 0.404 -> 0.393 ms)
     uint32_t i = hi - 1;
-    uint32_t gn = gs ? gs[i + 1] : 1u, g0 = gs ? gs[i] : 0u;
-    bool ne = g0 != gn;
-    G1Xyzz nx = ne ? load_xyzz(x, i) : G1Xyzz::identity();
+    G1Xyzz nx = G1Xyzz::identity();
+    bool ne = bucket_at(x, gs, i, nx);
     for (;;) {
       const G1Xyzz cur = nx;
       const bool cne = ne;
       const uint32_t ci = i;
       if (ci > lo) {
         i = ci - 1;
-        gn = g0;
-        g0 = gs ? gs[i] : gn + 1u;
-        ne = g0 != gn;
-        if (ne) nx = load_xyzz(x, i);
+        ne = bucket_at(x, gs, i, nx);
       }
       if (cne) run = xyzz_add(run, cur);
       if (base || ci > lo) acc = xyzz_add(acc, run);
@@ -895,7 +903,7 @@ static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, 
   SV_HIP(hipGetLastError());
   if (ev_sort_mid) SV_HIP(hipEventRecord(ev_sort_mid, st));
   hipLaunchKernelGGL(k_bin_scan_chunks, dim3(nwb), dim3(kBlock), 0, st, w.bcnt, nblk, w.btot);
-  hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, w.btot, nwb, w.bstart);
+  hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, w.btot, nwb, w.bstart, w.gst + p.nbt);
   SV_LAUNCH_C(k_bin_scatter, p.glv, p.c, dim3(nblk), dim3(kBlock), dsrc, npts, mont_in, nblk, w.bcnt, w.bstart,
               w.tmp);
   static thread_local int fine_attr_dev = -1;  // the > 64 KiB dynamic-LDS opt-in, once per thread/device
@@ -910,7 +918,6 @@ static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, 
                      w.tstart, w.ent);
   hipLaunchKernelGGL(k_fine_sort<true>, dim3(nwb), dim3(1024), kFineLds, st, w.tmp, w.bstart, FB, p.K, w.gst,
                      w.tstart, w.ent);
-  SV_HIP(hipMemcpyAsync(w.gst + p.nbt, w.bstart + nwb, 4, hipMemcpyDeviceToDevice, st));
   SV_HIP(hipGetLastError());
   if (bases_ready) SV_HIP(hipStreamWaitEvent(st, bases_ready, 0));
   if (conv_src)  // host-fed canonical bases: converted once they have landed, after the sort
@@ -918,7 +925,7 @@ static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, 
                        const_cast<G1Aff*>(bases), npts, w.err);
   if (ev_sorted) SV_HIP(hipEventRecord(ev_sorted, st));
   hipLaunchKernelGGL(k_accumulate, dim3(cdiv(T, kBlock)), dim3(kBlock), 0, st, bases, w.ent, w.gst, w.tstart,
-                     p.nbt, p.K, T, bsum, w.pfirst, w.plast, w.multi, w.nmulti, phi, nsplit);
+                     p.nbt, p.K, T, bsum, w.pfirst, w.plast, w.multi, w.nmulti, w.heavy, w.nheavy, phi, nsplit);
   SV_HIP(hipGetLastError());
   if (ev_acc_done) SV_HIP(hipEventRecord(ev_acc_done, st));
   hipLaunchKernelGGL(k_fixup_multi, dim3(std::min<uint32_t>(cdiv(p.nbt, kBlock), 1024)), dim3(kBlock), 0, st,

@@ -1,12 +1,16 @@
 // f2: the x^5 Poseidon sponge over BN254 Fr that drives PoseidonTranscript's Fiat-Shamir challenges
 // (snark-verifier/src/util/hash/poseidon.rs, system/halo2/transcript/halo2.rs:198-227).
 //
-// One lane per state.  The reference runs the "optimized" HADES schedule (poseidon.rs:121-208:
-// round-0 constants fused into absorb, sparse partial-round matrices); that schedule computes the
-// same map as the plain ARC -> S-box -> MDS rounds below, whose constants come from the Grain-LFSR
-// restatement in oracle/poseidon.py (pinned by the reference's permutation KATs, tests.rs:34-85)
-// and are compiled in as Montgomery limbs (poseidon_consts.hpp).  All constant loads are
-// wave-uniform (scalar loads); each lane's state stays in VGPRs.
+// One lane per state.  The permutation runs the reference's optimised HADES schedule
+// (OptimizedPoseidonSpec, poseidon.rs:230-313; Poseidon::permutation, :469-500): the round constants
+// folded through the inverse MDS (S-box then "+ constant"), a pre-sparse MDS after the first full
+// half, and in each of the R_P partial rounds a sparse matrix (row . state -> state[0], state[i] +=
+// col_hat[i-1] * state[0]) instead of the dense MDS: 2 t - 1 products per partial round instead of
+// t^2.  The constants come from oracle/poseidon.py's restatement of the Grain-LFSR generator and of
+// the reference's factorisation (tools/gen_consts.py -> poseidon_consts.hpp, Montgomery limbs); the
+// schedule computes the same map as the plain ARC -> S-box -> MDS rounds (pinned by the reference's
+// permutation KATs, tests.rs:34-85).  All constant loads are wave-uniform (scalar loads); each
+// lane's state stays in VGPRs.
 #include <hip/hip_runtime.h>
 
 #include "field.hpp"
@@ -16,24 +20,40 @@
 
 namespace sv {
 
-__constant__ uint32_t c_rc3[] = SV_POSEIDON_T3_RC_INIT;
+__constant__ uint32_t c_start3[] = SV_POSEIDON_T3_START_INIT;
+__constant__ uint32_t c_partial3[] = SV_POSEIDON_T3_PARTIAL_INIT;
+__constant__ uint32_t c_end3[] = SV_POSEIDON_T3_END_INIT;
 __constant__ uint32_t c_mds3[] = SV_POSEIDON_T3_MDS_INIT;
-__constant__ uint32_t c_rc5[] = SV_POSEIDON_T5_RC_INIT;
+__constant__ uint32_t c_pre3[] = SV_POSEIDON_T3_PRE_INIT;
+__constant__ uint32_t c_sparse3[] = SV_POSEIDON_T3_SPARSE_INIT;
+__constant__ uint32_t c_start5[] = SV_POSEIDON_T5_START_INIT;
+__constant__ uint32_t c_partial5[] = SV_POSEIDON_T5_PARTIAL_INIT;
+__constant__ uint32_t c_end5[] = SV_POSEIDON_T5_END_INIT;
 __constant__ uint32_t c_mds5[] = SV_POSEIDON_T5_MDS_INIT;
+__constant__ uint32_t c_pre5[] = SV_POSEIDON_T5_PRE_INIT;
+__constant__ uint32_t c_sparse5[] = SV_POSEIDON_T5_SPARSE_INIT;
 
 template <int T>
 struct PSpec;
 template <>
 struct PSpec<3> {
   static constexpr int RF = SV_POSEIDON_T3_RF, RP = SV_POSEIDON_T3_RP;
-  static __device__ __forceinline__ const uint32_t* rc() { return c_rc3; }
+  static __device__ __forceinline__ const uint32_t* start() { return c_start3; }
+  static __device__ __forceinline__ const uint32_t* partial() { return c_partial3; }
+  static __device__ __forceinline__ const uint32_t* end() { return c_end3; }
   static __device__ __forceinline__ const uint32_t* mds() { return c_mds3; }
+  static __device__ __forceinline__ const uint32_t* pre() { return c_pre3; }
+  static __device__ __forceinline__ const uint32_t* sparse() { return c_sparse3; }
 };
 template <>
 struct PSpec<5> {
   static constexpr int RF = SV_POSEIDON_T5_RF, RP = SV_POSEIDON_T5_RP;
-  static __device__ __forceinline__ const uint32_t* rc() { return c_rc5; }
+  static __device__ __forceinline__ const uint32_t* start() { return c_start5; }
+  static __device__ __forceinline__ const uint32_t* partial() { return c_partial5; }
+  static __device__ __forceinline__ const uint32_t* end() { return c_end5; }
   static __device__ __forceinline__ const uint32_t* mds() { return c_mds5; }
+  static __device__ __forceinline__ const uint32_t* pre() { return c_pre5; }
+  static __device__ __forceinline__ const uint32_t* sparse() { return c_sparse5; }
 };
 
 __device__ __forceinline__ Fr ld_const(const uint32_t* p) {
@@ -68,27 +88,47 @@ __device__ __forceinline__ Fr mds_row(const Fr (&s)[T], const uint32_t* row) {
   return acc;
 }
 
-// poseidon.rs:121-161 (permutation) == tests.rs's HADES reference: R_F/2 full, R_P partial, R_F/2 full.
+// s <- M s for a dense t x t matrix (rows of fused sums of products)
+template <int T>
+__device__ __forceinline__ void apply_mds(Fr (&s)[T], const uint32_t* m) {
+  Fr o[T];
+#pragma unroll
+  for (int i = 0; i < T; i++) o[i] = mds_row<T>(s, m + i * T * 8);
+#pragma unroll
+  for (int i = 0; i < T; i++) s[i] = o[i];
+}
+
+// full round: s_i <- s_i^5 + c_i (State::sbox_full, poseidon.rs:353-357), then the dense matrix
+template <int T>
+__device__ __forceinline__ void full_round(Fr (&s)[T], const uint32_t* c, const uint32_t* m) {
+#pragma unroll
+  for (int i = 0; i < T; i++) s[i] = c ? pow5(s[i]) + ld_const(c + i * 8) : pow5(s[i]);
+  apply_mds<T>(s, m);
+}
+
+// Poseidon::permutation (poseidon.rs:469-500) without the absorbed inputs: the bare HADES map.
 template <int T>
 __device__ __forceinline__ void permute(Fr (&s)[T]) {
-  constexpr int RF = PSpec<T>::RF, RP = PSpec<T>::RP;
-  const uint32_t* rc = PSpec<T>::rc();
-  const uint32_t* mds = PSpec<T>::mds();
-  for (int r = 0; r < RF + RP; r++) {
+  constexpr int RF = PSpec<T>::RF, RP = PSpec<T>::RP, H = RF / 2;
+  const uint32_t* start = PSpec<T>::start();
 #pragma unroll
-    for (int i = 0; i < T; i++) s[i] = s[i] + ld_const(rc + (r * T + i) * 8);
-    if (r < RF / 2 || r >= RF / 2 + RP) {
+  for (int i = 0; i < T; i++) s[i] = s[i] + ld_const(start + i * 8);  // absorb_with_pre_constants
+  for (int r = 1; r < H; r++) full_round<T>(s, start + r * T * 8, PSpec<T>::mds());
+  full_round<T>(s, start + H * T * 8, PSpec<T>::pre());
+  // partial rounds: sbox_part, then apply_sparse_mds (poseidon.rs:359-361, :399-412)
+  const uint32_t* partial = PSpec<T>::partial();
+  const uint32_t* sparse = PSpec<T>::sparse();
+  for (int r = 0; r < RP; r++) {
+    s[0] = pow5(s[0]) + ld_const(partial + r * 8);
+    const uint32_t* row = sparse + r * (2 * T - 1) * 8;
+    const Fr s0 = mds_row<T>(s, row);
 #pragma unroll
-      for (int i = 0; i < T; i++) s[i] = pow5(s[i]);
-    } else {
-      s[0] = pow5(s[0]);
-    }
-    Fr o[T];
-#pragma unroll
-    for (int i = 0; i < T; i++) o[i] = mds_row<T>(s, mds + i * T * 8);
-#pragma unroll
-    for (int i = 0; i < T; i++) s[i] = o[i];
+    for (int i = 1; i < T; i++) s[i] = s[i] + s[0] * ld_const(row + (T + i - 1) * 8);
+    s[0] = s0;
   }
+  const uint32_t* end = PSpec<T>::end();
+  for (int r = 0; r < H - 1; r++) full_round<T>(s, end + r * T * 8, PSpec<T>::mds());
+  full_round<T>(s, nullptr, PSpec<T>::mds());
 }
 
 __device__ __forceinline__ Fr load_fr(const Fr* p, int mont) {

@@ -44,6 +44,23 @@ def test_poseidon_permutation_kat(key):
     assert poseidon.permutation(k["input"], k["t"], k["r_f"], k["r_p"]) == [int(v) for v in k["output"]]
 
 
+@pytest.mark.parametrize("key", ["perm_x5_254_3", "perm_x5_254_5"])
+def test_poseidon_optimized_schedule_matches_kat_and_plain(key):
+    """The reference's optimised schedule (OptimizedPoseidonSpec: folded constants, pre-sparse MDS,
+    sparse partial-round matrices, poseidon.rs:170-328 / :469-500), restated in oracle/poseidon.py
+    and compiled into the GPU kernel, reproduces the KAT and the plain HADES rounds."""
+    import random
+    k = load_golden("poseidon_kat.json")[key]
+    t, rf, rp = k["t"], k["r_f"], k["r_p"]
+    assert poseidon.permutation_optimized(k["input"], t, rf, rp) == [int(v) for v in k["output"]]
+    rng = random.Random(t)
+    for _ in range(4):
+        st = [rng.randrange(poseidon.FR_MODULUS) for _ in range(t)]
+        assert poseidon.permutation_optimized(st, t, rf, rp) == poseidon.permutation(st, t, rf, rp)
+    sp = poseidon.optimized_spec(t, rf, rp)
+    assert len(sp["sparse"]) == rp and len(sp["start"]) == rf // 2 + 1 and len(sp["end"]) == rf // 2 - 1
+
+
 def test_pairing_tower_equals_generic_formulation():
     e = b.pairing(b.G1_GEN, b.G2_GEN)
     assert b.tower_to_poly(e) == b.pairing_generic(b.G1_GEN, b.G2_GEN)

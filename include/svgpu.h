@@ -147,7 +147,16 @@ int sv_bn254_g1_table_destroy(uint64_t handle) SV_NOEXCEPT;
 int sv_bn254_g1_msm_batch_table(uint64_t handle, const uint32_t* base_idx, const sv_fe* scalars,
                                 const uint64_t* offsets, size_t count, int form,
                                 sv_g1_affine* out) SV_NOEXCEPT;
-/* device-buffer form: d_table (table_len rows, `table_form`), d_base_idx / d_scalars / d_offsets /
+/* Table rows are precomputed at creation as their window multiples 2^(8 w) P (w < 32, affine,
+ * 2 KiB per row on the device), so a table-backed MSM puts every signed 8-bit digit of every
+ * term into ONE bucket set (no per-MSM Horner over windows).  Device-buffer form of the same:
+ * d_base_idx / d_scalars / d_offsets (count + 1 entries) / d_out on the table's device
+ * (sv_bn254_g1_table_device), synchronous on `stream`; an empty MSM gives the identity.     */
+int sv_bn254_g1_msm_batch_table_device(uint64_t handle, const uint32_t* d_base_idx, const sv_fe* d_scalars,
+                                       const uint64_t* d_offsets, size_t count, int form, void* stream,
+                                       sv_g1_affine* d_out) SV_NOEXCEPT;
+int sv_bn254_g1_table_device(uint64_t handle, int* device) SV_NOEXCEPT;
+/* device-buffer form over a raw (not precomputed) table: d_table (table_len rows, `table_form`), d_base_idx / d_scalars / d_offsets /
  * d_out on `device`; max_terms = the largest MSM (picks the window size); synchronous.        */
 int sv_bn254_g1_msm_batch_indexed_device(const sv_g1_affine* d_table, size_t table_len, int table_form,
                                          const uint32_t* d_base_idx, const sv_fe* d_scalars,

@@ -522,7 +522,8 @@ int sv_bn254_g1_msm_batch_device(const sv_g1_affine* d_bases, const sv_fe* d_sca
 namespace {
 struct BaseTable {
   int dev = 0;
-  void* p = nullptr;
+  void* p = nullptr;    // rows (Montgomery affine)
+  void* pre = nullptr;  // rows expanded to their window multiples 2^(8 w) P (msm_batch_fixed_device)
   size_t n = 0;
 };
 std::mutex g_tables_mu;
@@ -590,10 +591,19 @@ int sv_bn254_g1_table_create(const sv_g1_affine* bases, size_t n, int form, int 
   t.n = n;
   SV_HIP(hipSetDevice(dev));
   SV_HIP(hipMalloc(&t.p, n * sizeof(sv_g1_affine)));
-  if (hipMemcpy(t.p, mont.data(), n * sizeof(sv_g1_affine), hipMemcpyHostToDevice) != hipSuccess) {
-    hipFree(t.p);
-    sv::set_error("base table upload failed");
-    return SV_ERR_DEVICE;
+  if (hipMalloc(&t.pre, table_precomputed_rows_bytes(n)) != hipSuccess) {
+    (void)hipFree(t.p);
+    sv::set_error("base table: precomputed rows hipMalloc failed");
+    return SV_ERR_OOM;
+  }
+  int prc = hipMemcpy(t.p, mont.data(), n * sizeof(sv_g1_affine), hipMemcpyHostToDevice) == hipSuccess
+                ? table_precompute_device(t.p, n, t.pre, dev)
+                : SV_ERR_DEVICE;
+  if (prc != SV_OK) {
+    (void)hipFree(t.p);
+    (void)hipFree(t.pre);
+    sv::set_error("base table upload / precompute failed");
+    return prc;
   }
   std::lock_guard<std::mutex> lk(g_tables_mu);
   *handle = g_next_table++;
@@ -617,6 +627,7 @@ int sv_bn254_g1_table_destroy(uint64_t handle) noexcept {
   }
   SV_HIP(hipSetDevice(t.dev));
   SV_HIP(hipFree(t.p));
+  SV_HIP(hipFree(t.pre));
   return SV_OK;
   SV_GUARD_END
 }
@@ -653,10 +664,41 @@ int sv_bn254_g1_msm_batch_table(uint64_t handle, const uint32_t* base_idx, const
   SV_TRY(sg.put(1, scalars + base, total * sizeof(sv_fe)));
   SV_TRY(sg.put(2, off.data(), (count + 1) * sizeof(uint64_t)));
   SV_TRY(sg.sync());
-  SV_TRY(msm_batch_device(t.p, sg.at(1), sg.at<const uint64_t>(2), nullptr, count, max_terms, form, t.dev, nullptr,
-                          sg.at(3), sg.at<const uint32_t>(0), t.n, SV_MONTGOMERY));
+  (void)max_terms;
+  SV_TRY(msm_batch_fixed_device(t.pre, t.n, sg.at<const uint32_t>(0), sg.at(1), sg.at<const uint64_t>(2), count, form,
+                                t.dev, nullptr, sg.at(3)));
   SV_TRY(sg.get(out, 3, count * sizeof(sv_g1_affine)));
   SV_TRY(sg.sync());
+  return SV_OK;
+  SV_GUARD_END
+}
+
+int sv_bn254_g1_msm_batch_table_device(uint64_t handle, const uint32_t* d_base_idx, const sv_fe* d_scalars,
+                                       const uint64_t* d_offsets, size_t count, int form, void* stream,
+                                       sv_g1_affine* d_out) noexcept {
+  SV_GUARD_BEGIN
+  SV_TRY(check_form(form));
+  if (count == 0) return SV_OK;
+  if (!d_base_idx || !d_scalars || !d_offsets || !d_out) return SV_ERR_ARG;
+  BaseTable t;
+  if (!table_lookup(handle, &t)) {
+    sv::set_error("unknown base table handle %llu", (unsigned long long)handle);
+    return SV_ERR_ARG;
+  }
+  SV_HIP(hipSetDevice(t.dev));
+  return msm_batch_fixed_device(t.pre, t.n, d_base_idx, d_scalars, d_offsets, count, form, t.dev,
+                                (hipStream_t)stream, d_out);
+  SV_GUARD_END
+}
+
+int sv_bn254_g1_table_device(uint64_t handle, int* device) noexcept {
+  SV_GUARD_BEGIN
+  BaseTable t;
+  if (!device || !table_lookup(handle, &t)) {
+    sv::set_error("unknown base table handle %llu", (unsigned long long)handle);
+    return SV_ERR_ARG;
+  }
+  *device = t.dev;
   return SV_OK;
   SV_GUARD_END
 }

@@ -358,6 +358,160 @@ __global__ void __launch_bounds__(64) k_msm_batch_horner(const G1Xyzz* __restric
   }
 }
 
+// ---- Precomputed fixed bases (base tables) -------------------------------------
+// A table row P is stored as its window multiples Q_w = 2^(8 w) P, w < kFixW (affine, Montgomery),
+// so sum_i k_i P_i = sum_i sum_w d_iw Q_iw: every signed 8-bit digit of every term lands in ONE set
+// of 128 buckets and the per-MSM Horner chain over windows disappears.  One 256-thread block per
+// MSM: digits -> LDS counting sort by bucket (chunks of kFixChunk terms), two threads per bucket
+// sum their half of its entries with mixed adds, then sum_b (b + 1) S_b = sum_k T_k over the
+// suffix sums T_k = sum_{b >= k} S_b: a 7-level LDS scan and a 7-level tree (depth 14 instead of the
+// ~128 dependent doublings of the window Horner), and one inversion for the affine output.
+constexpr int kFixC = 8;
+constexpr int kFixB = 1 << (kFixC - 1);                  // 128 buckets (signed digits)
+constexpr int kFixW = (255 + kFixC - 1) / kFixC;         // 32 windows cover scalars < r < 2^254
+constexpr int kFixChunk = 256;                           // terms per LDS pass
+
+// one thread per row: Q_w = 2^(8 w) P (identity rows stay (0, 0))
+__global__ void __launch_bounds__(kThreads) k_table_precompute(const G1Aff* __restrict__ rows, uint32_t n,
+                                                               G1Aff* __restrict__ pre) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* rp = reinterpret_cast<const uint32_t*>(rows + i);
+  const Fq x = ld_fq(rp), y = ld_fq(rp + 8);
+  uint32_t* o = reinterpret_cast<uint32_t*>(pre + (size_t)i * kFixW);
+  if (x.is_zero() && y.is_zero()) {
+    for (int w = 0; w < kFixW; w++) {
+      st_fq(o + 16 * w, Fq::zero());
+      st_fq(o + 16 * w + 8, Fq::zero());
+    }
+    return;
+  }
+  G1Xyzz acc = {x, y, Fq::one(), Fq::one()};
+  for (int w = 0; w < kFixW; w++) {
+    if (w) {
+      for (int d = 0; d < kFixC; d++) acc = xyzz_dbl(acc);
+    }
+    const G1Aff a = xyzz_to_affine(acc);  // never the identity: P has prime order r > 2^(8 w)
+    st_fq(o + 16 * w, a.x);
+    st_fq(o + 16 * w + 8, a.y);
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) k_msm_batch_fixed(const G1Aff* __restrict__ pre, uint32_t rows,
+                                                              const uint32_t* __restrict__ bidx,
+                                                              const Fr* __restrict__ scalars,
+                                                              const uint64_t* __restrict__ off, int mont,
+                                                              G1Aff* __restrict__ out, uint32_t* __restrict__ err) {
+  __shared__ uint32_t cnt[kFixB];                 // histogram, then scatter cursors
+  __shared__ uint32_t bst[kFixB + 1];             // bucket starts in lst
+  __shared__ uint32_t lst[kFixChunk * kFixW];     // (row * kFixW + w) << 1 | sign, sorted by bucket
+  __shared__ uint8_t dig[kFixChunk * kFixW];      // magnitude of digit (term, w); sign in sgn
+  __shared__ uint32_t sgn[kFixChunk];             // sign bits of the term's kFixW digits
+  __shared__ G1Xyzz T[kFixB];
+  const int tid = threadIdx.x;
+  const uint32_t id = blockIdx.x;
+  const uint64_t b0 = off[id], e0 = off[id + 1];
+  const int bucket = tid % kFixB, part = tid / kFixB;  // 2 threads per bucket
+  G1Xyzz acc = G1Xyzz::identity();
+  for (uint64_t c0 = b0; c0 < e0; c0 += kFixChunk) {
+    const int m = (int)(e0 - c0 < (uint64_t)kFixChunk ? e0 - c0 : (uint64_t)kFixChunk);
+    if (tid < kFixB) cnt[tid] = 0;
+    __syncthreads();
+    uint32_t row = 0;
+    if (tid < m) {
+      Fr s;
+      {
+        const Fq t = ld_fq(reinterpret_cast<const uint32_t*>(scalars + c0 + tid));
+#pragma unroll
+        for (int i = 0; i < 8; i++) s.v[i] = t.v[i];
+      }
+      if (!s.is_reduced()) atomicOr(err, 2u);
+      if (mont) s = fe_from_mont(s);
+      row = bidx[c0 + tid];
+      if (row >= rows) {
+        atomicOr(err, 4u);
+        s = Fr::zero();
+      }
+      uint32_t carry = 0, sg = 0;
+      for (int w = 0; w < kFixW; w++) {  // signed 8-bit digits in (-128, 128]
+        const uint32_t bits = ((s.v[w >> 2] >> ((w & 3) * 8)) & 0xffu) + carry;
+        uint32_t mag;
+        if (bits > (uint32_t)kFixB) {
+          mag = 256u - bits;  // bits == 256: digit 0, carry 1
+          if (mag) sg |= 1u << w;
+          carry = 1;
+        } else {
+          mag = bits;
+          carry = 0;
+        }
+        dig[tid * kFixW + w] = (uint8_t)mag;
+        if (mag) atomicAdd(&cnt[mag - 1], 1u);
+      }
+      sgn[tid] = sg;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t a = 0;
+      for (int b = 0; b < kFixB; b++) {
+        bst[b] = a;
+        a += cnt[b];
+        cnt[b] = bst[b];
+      }
+      bst[kFixB] = a;
+    }
+    __syncthreads();
+    if (tid < m) {
+      const uint32_t sg = sgn[tid];
+      for (int w = 0; w < kFixW; w++) {
+        const uint32_t mag = dig[tid * kFixW + w];
+        if (mag) lst[atomicAdd(&cnt[mag - 1], 1u)] = ((row * kFixW + w) << 1) | ((sg >> w) & 1u);
+      }
+    }
+    __syncthreads();
+    for (uint32_t q = bst[bucket] + part; q < bst[bucket + 1]; q += 2) {
+      const uint32_t e = lst[q];
+      const uint32_t* qp = reinterpret_cast<const uint32_t*>(pre + (e >> 1));
+      G1Aff a;
+      a.x = ld_fq(qp);
+      a.y = ld_fq(qp + 8);
+      if (a.x.is_zero() && a.y.is_zero()) continue;  // identity row
+      if (e & 1) a.y = -a.y;
+      acc = xyzz_madd_aff(acc, a);
+    }
+    __syncthreads();
+  }
+  // S_b = the two halves of bucket b
+  if (part == 1) T[bucket] = acc;
+  __syncthreads();
+  if (part == 0) T[bucket] = xyzz_add(acc, T[bucket]);
+  __syncthreads();
+  // suffix sums T_k = sum_{b >= k} S_b (Hillis-Steele, 7 levels)
+  for (int d = 1; d < kFixB; d <<= 1) {
+    G1Xyzz v = G1Xyzz::identity();
+    const bool live = tid < kFixB && tid + d < kFixB;
+    if (live) v = T[tid + d];
+    __syncthreads();
+    if (live) T[tid] = xyzz_add(T[tid], v);
+    __syncthreads();
+  }
+  // sum_b (b + 1) S_b = sum_k T_k (tree, 7 levels)
+  for (int h = kFixB / 2; h >= 1; h >>= 1) {
+    if (tid < h) T[tid] = xyzz_add(T[tid], T[tid + h]);
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const G1Xyzz r = T[0];
+    G1Aff a = xyzz_to_affine(r);
+    if (!mont && !r.is_identity()) {
+      a.x = fe_from_mont(a.x);
+      a.y = fe_from_mont(a.y);
+    }
+    uint32_t* o = reinterpret_cast<uint32_t*>(out + id);
+    st_fq(o, a.x);
+    st_fq(o + 8, a.y);
+  }
+}
+
 }  // namespace
 
 int msm_batch_window_bits(size_t max_terms) {
@@ -418,6 +572,59 @@ int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t*
   }
   if (ev & 4u) {
     set_error("msm_batch: base index out of the table (>= %llu)", (unsigned long long)table_len);
+    return SV_ERR_ARG;
+  }
+  return SV_OK;
+}
+
+}  // namespace sv
+
+namespace sv {
+
+size_t table_precomputed_rows_bytes(size_t n) { return n * (size_t)kFixW * sizeof(G1Aff); }
+
+int table_precompute_device(const void* d_rows, size_t n, void* d_pre, int device) {
+  if (n == 0) return SV_OK;
+  WsLease lease(device, nullptr);
+  if (!lease.ok()) return SV_ERR_DEVICE;
+  hipStream_t st = lease.get()->stream;
+  hipLaunchKernelGGL(k_table_precompute, dim3((uint32_t)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0, st,
+                     static_cast<const G1Aff*>(d_rows), (uint32_t)n, static_cast<G1Aff*>(d_pre));
+  SV_HIP(hipGetLastError());
+  SV_HIP(hipStreamSynchronize(st));
+  return SV_OK;
+}
+
+int msm_batch_fixed_device(const void* d_pre, size_t rows, const uint32_t* d_bidx, const void* d_scalars,
+                           const uint64_t* d_offsets, size_t count, int form, int device, hipStream_t stream,
+                           void* d_out) {
+  if (count == 0) return SV_OK;
+  if (count > 0x7fffffffull) {
+    set_error("msm_batch: count = %zu too large", count);
+    return SV_ERR_LEN;
+  }
+  WsLease lease(device, stream);
+  if (!lease.ok()) return SV_ERR_DEVICE;
+  Workspace* ws = lease.get();
+  hipStream_t st = ws->stream;
+  SV_TRY(ws->reserve(Workspace::aligned(4)));
+  SV_TRY(ws->reserve_pinned(256));
+  uint32_t* err = ws->carve<uint32_t>(1);
+  SV_HIP(hipMemsetAsync(err, 0, 4, st));
+  hipLaunchKernelGGL(k_msm_batch_fixed, dim3((uint32_t)count), dim3(kThreads), 0, st, static_cast<const G1Aff*>(d_pre),
+                     (uint32_t)rows, d_bidx, static_cast<const Fr*>(d_scalars), d_offsets,
+                     form == SV_MONTGOMERY ? 1 : 0, static_cast<G1Aff*>(d_out), err);
+  SV_HIP(hipGetLastError());
+  SV_HIP(hipMemcpyAsync(ws->pinned, err, 4, hipMemcpyDeviceToHost, st));
+  SV_HIP(hipStreamSynchronize(st));
+  uint32_t ev;
+  memcpy(&ev, ws->pinned, 4);
+  if (ev & 2u) {
+    set_error("msm_batch: scalar not reduced (>= r)");
+    return SV_ERR_ARG;
+  }
+  if (ev & 4u) {
+    set_error("msm_batch: base index out of the table (>= %zu)", rows);
     return SV_ERR_ARG;
   }
   return SV_OK;

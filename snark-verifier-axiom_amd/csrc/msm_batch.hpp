@@ -16,4 +16,14 @@ int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t*
                      size_t count, size_t max_terms, int form, int device, hipStream_t stream, void* d_out,
                      const uint32_t* d_bidx = nullptr, uint64_t table_len = 0, int base_form = 0);
 int msm_batch_window_bits(size_t max_terms);
+
+// Precomputed base tables: every row P expanded to its window multiples 2^(8 w) P (affine,
+// Montgomery) so that table-backed MSMs need one bucket set and no window Horner.
+size_t table_precomputed_rows_bytes(size_t n);
+int table_precompute_device(const void* d_rows, size_t n, void* d_pre, int device);
+// MSM k = sum over i in [off[k], off[k+1]) of scalars[i] * table[bidx[i]] from the precomputed rows;
+// an empty MSM gives the identity; index >= rows or an unreduced scalar is SV_ERR_ARG.  Synchronous.
+int msm_batch_fixed_device(const void* d_pre, size_t rows, const uint32_t* d_bidx, const void* d_scalars,
+                           const uint64_t* d_offsets, size_t count, int form, int device, hipStream_t stream,
+                           void* d_out);
 }  // namespace sv

@@ -104,6 +104,9 @@ PROTOTYPES = [
     ("sv_bn254_g1_table_create", c_int, [c_void_p, c_size_t, c_int, c_int, POINTER(c_uint64)]),
     ("sv_bn254_g1_table_destroy", c_int, [c_uint64]),
     ("sv_bn254_g1_msm_batch_table", c_int, [c_uint64, c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
+    ("sv_bn254_g1_msm_batch_table_device", c_int, [c_uint64, c_void_p, c_void_p, c_void_p, c_size_t, c_int,
+                                                    c_void_p, c_void_p]),
+    ("sv_bn254_g1_table_device", c_int, [c_uint64, POINTER(c_int)]),
     ("sv_bn254_g1_msm_batch_indexed_device", c_int, [c_void_p, c_size_t, c_int, c_void_p, c_void_p, c_void_p,
                                                       c_size_t, c_size_t, c_int, c_int, c_void_p, c_void_p]),
     ("sv_bn254_poseidon_permute", c_int, [c_void_p, c_size_t, c_int, c_int]),

@@ -99,7 +99,9 @@ class BaseTable:
     """Device-resident fixed bases (the generator and a circuit's preprocessed commitments, loaded
     once per verifier: Protocol::loaded, plonk/protocol.rs:106-131) referenced by row index from
     each proof's MSMs (Msm::evaluate, bdfg21.rs:75-78 / gwc19.rs:76-79), so a per-proof batch ships
-    only scalars and u32 indices.  Rows are uploaded once in Montgomery form on `device`."""
+    only scalars and u32 indices.  Rows are uploaded once in Montgomery form on `device` and expanded
+    there to their window multiples 2^(8 w) P, so every batch runs in one bucket set per MSM with
+    no window Horner (csrc/msm_batch.hip k_msm_batch_fixed)."""
 
     def __init__(self, bases, device: int = 0):
         if not isinstance(bases, np.ndarray):
@@ -151,6 +153,26 @@ class BaseTable:
             raise ReferencePanic("pairs should not be empty")
         _lib.check(rc, "sv_bn254_g1_msm_batch_table")
         return [enc.g1_from_struct(o, form) for o in out]
+
+    def device(self) -> int:
+        d = ctypes.c_int(-1)
+        _lib.check(_lib.lib.sv_bn254_g1_table_device(self.handle, ctypes.byref(d)), "sv_bn254_g1_table_device")
+        return d.value
+
+    def msm_batch_device(self, base_idx, scalars, offsets, form: int = _lib.SV_MONTGOMERY, out=None):
+        """HBM-resident form (torch tensors on the table's device): base_idx (terms,) int32, scalars
+        (terms, 4) int64, offsets (count + 1,) int64 -> (count, 8) int64 affine results in `form`."""
+        import torch
+        if self.handle is None:
+            raise _lib.ArgumentError("base table is closed")
+        count = offsets.shape[0] - 1
+        if out is None:
+            out = torch.empty((max(count, 1), 8), dtype=torch.int64, device=scalars.device)
+        stream = torch.cuda.current_stream(scalars.device).cuda_stream
+        _lib.check(_lib.lib.sv_bn254_g1_msm_batch_table_device(self.handle, base_idx.data_ptr(), scalars.data_ptr(),
+                                                                offsets.data_ptr(), count, form, stream,
+                                                                out.data_ptr()), "sv_bn254_g1_msm_batch_table_device")
+        return out[:count]
 
     def batch_multi_scalar_multiplication(self, msms: Sequence[Sequence[Tuple[int, int]]]) -> list:
         """msms: per MSM a list of (scalar, table row) pairs."""

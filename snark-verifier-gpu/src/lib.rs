@@ -118,6 +118,10 @@ extern "C" {
     pub fn sv_bn254_g1_msm_batch_table(handle: u64, base_idx: *const u32, scalars: *const SvFe,
                                        offsets: *const u64, count: usize, form: c_int,
                                        out: *mut SvG1Affine) -> c_int;
+    pub fn sv_bn254_g1_msm_batch_table_device(handle: u64, d_base_idx: *const u32, d_scalars: *const SvFe,
+                                              d_offsets: *const u64, count: usize, form: c_int, stream: *mut c_void,
+                                              d_out: *mut SvG1Affine) -> c_int;
+    pub fn sv_bn254_g1_table_device(handle: u64, device: *mut c_int) -> c_int;
     pub fn sv_bn254_g1_msm_batch_indexed_device(d_table: *const SvG1Affine, table_len: usize, table_form: c_int,
                                                 d_base_idx: *const u32, d_scalars: *const SvFe,
                                                 d_offsets: *const u64, count: usize, max_terms: usize,

@@ -178,3 +178,51 @@ def test_unreduced_base_rejected_on_both_routes(gpu, oracle_cpp, monkeypatch, se
     B[13, 0:4] = np.array([0xffffffffffffffff] * 4, np.uint64)  # x = 2^256 - 1 >= p
     with pytest.raises(svgpu.ArgumentError):
         svgpu.msm_batch_arrays(B, S, off)
+
+
+def test_precomputed_table_device_api(gpu, oracle_cpp):
+    """Precomputed table rows (2^(8w) P per row, one bucket set per MSM, k_msm_batch_fixed) through
+    the HBM-resident handle API: 128 MSMs x 64 terms over a 4096-row table, both forms, against
+    the reference Pippenger over the gathered bases; then the edge terms (identity row, zero and
+    r - 1 scalars, repeated rows, > 256 terms: several LDS chunks) and an out-of-table index."""
+    import svgpu
+    from svgpu import encoding as enc
+    rows, count, m = 4096, 128, 64
+    n = count * m
+    Th = oracle_cpp.gen_bases(b.SEED_BASES, rows, start=777)
+    Sh = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=777)
+    rng = np.random.default_rng(5)
+    ih = rng.integers(0, rows, n).astype(np.uint32)
+    offs = list(range(0, n + 1, m))
+    exp = _expected(oracle_cpp, Th[ih], Sh, offs)
+    with svgpu.BaseTable(Th) as tab:
+        assert tab.device() == 0
+        idx = torch.from_numpy(ih.view(np.int32)).to(gpu)
+        off = torch.tensor(offs, dtype=torch.int64, device=gpu)
+        Sc = torch.from_numpy(Sh.view(np.int64)).to(gpu)
+        got = tab.msm_batch_device(idx, Sc, off, svgpu.SV_CANONICAL)
+        torch.cuda.synchronize()
+        assert [enc.g1_from_limbs(r) for r in got.cpu().numpy().view(np.uint64)] == exp
+        Sm = torch.from_numpy(enc.scalars_array([enc.limbs_to_int(r) for r in Sh[:8 * m]],
+                                                svgpu.SV_MONTGOMERY).view(np.int64)).to(gpu)
+        gm = tab.msm_batch_device(idx[:8 * m], Sm, off[:9], svgpu.SV_MONTGOMERY)
+        assert [enc.g1_from_limbs(r, svgpu.SV_MONTGOMERY) for r in gm.cpu().numpy().view(np.uint64)] == exp[:8]
+        bad = idx.clone()
+        bad[77] = rows
+        with pytest.raises(svgpu.ArgumentError):
+            tab.msm_batch_device(bad, Sc, off, svgpu.SV_CANONICAL)
+    T2 = Th[:40].copy()
+    T2[3] = 0                                            # identity row
+    with svgpu.BaseTable(T2) as tab:
+        P = [enc.g1_from_limbs(r) for r in T2]
+        msms = [
+            [(0, 1), (0, 2)],                            # -> identity
+            [(5, 3), (9, 4)],                            # identity row
+            [(b.R - 1, 6), (1, 6)],                      # (r - 1) P + P = O
+            [(11, 7)] * 50,                              # repeated row
+            [(1 << k, 8) for k in range(0, 254, 3)],     # powers of two, top windows
+            [(int(rng.integers(1, 1 << 62)) * (k + 1) % b.R, k % 40) for k in range(700)],  # 3 LDS chunks
+        ]
+        got = tab.batch_multi_scalar_multiplication(msms)
+        for pairs, g in zip(msms, got):
+            assert g == b.native_msm([s for s, _ in pairs], [P[i] for _, i in pairs])

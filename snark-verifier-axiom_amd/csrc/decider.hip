@@ -559,6 +559,474 @@ __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ l
   }
 }
 
+// =============================================================================================
+// Workgroup decider (default): one 256-thread block -- four waves, one per SIMD of a CU -- per
+// accumulator.  The single-wave kernel above keeps one SIMD busy per accumulator, so 256
+// accumulators leave three quarters of the chip's 1024 SIMDs idle, and each of its lanes runs two or
+// three dependent Fq products per Fq12 operation (~0.65 us each on one wave).  Here every Fq12
+// operation spreads its Fq products over the block, ONE product per lane:
+//   w_mul   144 lanes (6 output coefficients x 6 terms x 4 schoolbook Fq2 partial products),
+//   w_sqr    96 lanes (6 coefficients x <= 4 pair terms x <= 4 partial products),
+//   w_frob   24 lanes (6 coefficients x 4),
+// each lane scales its product by its place in the result (the w^6 = xi wrap multiplies by 9 + u),
+// and a coefficient's lanes add up with cross-lane moves (DPP quad/half-row/row mirrors, one
+// ds_swizzle for the 32-lane level) -- no LDS round trip inside an operation.  Operands and results
+// live in LDS slots of 6 Fq2 (the w-basis of fq12_lanes.hpp); an operation never writes a slot it
+// reads (one barrier per operation).  The operations are out-of-line functions: one copy of each
+// in the code object instead of ~60 inlined ones (instruction-cache footprint).  The Miller loop (merged step multipliers) and the final
+// exponentiation are the chain of k_decide_lanes, written over slots.
+// =============================================================================================
+#ifndef SV_WG_FN
+#define SV_WG_FN __device__ __forceinline__
+#endif
+namespace wg {
+constexpr int kThreads = 256;
+
+template <int L>
+__device__ __forceinline__ uint32_t xmove(uint32_t x) {
+  if constexpr (L == 0) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);   // lane ^ 1
+  else if constexpr (L == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // lane ^ 2
+  else if constexpr (L == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // 7 - i in 8
+  else if constexpr (L == 3) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);  // 15 - i in 16
+  else return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);  // lane ^ 16 (bit mode, within 32)
+}
+// Lazily reduced sums: a lane's contribution and the cross-lane partial sums are plain 9-limb
+// integers (every sum here stays below 300 p < 2^263), reduced mod p ONCE per coefficient -- a
+// cross-lane level then costs one 9-limb carry chain instead of a modular addition, and the xi
+// factor 9 is a shift and an add.
+struct Lz {
+  uint32_t v[9];
+};
+__device__ __forceinline__ Lz lz(const Fq& a) {
+  Lz r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = a.v[i];
+  r.v[8] = 0;
+  return r;
+}
+__device__ __forceinline__ Lz lz_zero() {
+  Lz r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = 0;
+  return r;
+}
+__device__ __forceinline__ Lz lz_add(const Lz& a, const Lz& b) {
+  Lz r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+  return r;
+}
+__device__ __forceinline__ Lz lz_mul9(const Lz& a) {  // (a << 3) + a
+  Lz s;
+  s.v[0] = a.v[0] << 3;
+#pragma unroll
+  for (int i = 1; i < 9; i++) s.v[i] = __builtin_amdgcn_alignbit(a.v[i], a.v[i - 1], 29);
+  return lz_add(s, a);
+}
+// a mod p for a < 2^264, to [0, 2p): k = floor(a / p) from the top 40 bits (exact in double; never
+// above the true quotient, at most one below), a - k p.  Slots hold such partially reduced values:
+// the Montgomery product is exact for inputs below 2p (4 p^2 < 2^256 p) and returns them reduced.
+__device__ __forceinline__ Fq lz_reduce(const Lz& a) {
+  const uint64_t hi = ((uint64_t)a.v[8] << 32) | a.v[7];  // a >> 224
+  const uint32_t k = (uint32_t)((double)hi / (double)(FQ_P[7] + 1ull));
+  uint32_t r[9];
+  uint32_t br = 0;
+  uint64_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t kp = (uint64_t)k * FQ_P[i] + carry;  // v_mad_u64_u32
+    carry = kp >> 32;
+    r[i] = __builtin_subc(a.v[i], (uint32_t)kp, br, &br);
+  }
+  Fq t;
+#pragma unroll
+  for (int i = 0; i < 8; i++) t.v[i] = r[i];
+  return t;
+}
+// [0, 2p) -> fully reduced
+__device__ __forceinline__ Fq fq_canon(const Fq& a) {
+  Fq d;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) d.v[i] = __builtin_subc(a.v[i], FQ_P[i], br, &br);
+  return br ? a : d;
+}
+__device__ __forceinline__ Fq2 fq2_canon(const Fq2& a) { return {fq_canon(a.c0), fq_canon(a.c1)}; }
+// 2p - a for a in [0, 2p]: the negation of a partially reduced value
+__device__ __forceinline__ Fq fq_neg2p(const Fq& a) {
+  static constexpr uint32_t P2[8] = {0xb0f9fa8eu, 0x7841182du, 0xd0e3951au, 0x2f02d522u,
+                                     0x0302b0bbu, 0x70a08b6du, 0xc2634053u, 0x60c89ce5u};
+  Fq r;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = __builtin_subc(P2[i], a.v[i], br, &br);
+  return r;
+}
+template <int L>
+__device__ __forceinline__ Lz xmove(const Lz& a) {
+  Lz r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = xmove<L>(a.v[i]);
+  return r;
+}
+// (re, im) summed over aligned groups of 2^LEVELS lanes; every lane of a group ends with the sum
+// (after levels 0 and 1 a quad is uniform, so the mirrors of levels 2 and 3 reach the other half)
+template <int LEVELS>
+__device__ __forceinline__ void lane_sum(Lz& re, Lz& im) {
+  if constexpr (LEVELS > 0) { re = lz_add(re, xmove<0>(re)); im = lz_add(im, xmove<0>(im)); }
+  if constexpr (LEVELS > 1) { re = lz_add(re, xmove<1>(re)); im = lz_add(im, xmove<1>(im)); }
+  if constexpr (LEVELS > 2) { re = lz_add(re, xmove<2>(re)); im = lz_add(im, xmove<2>(im)); }
+  if constexpr (LEVELS > 3) { re = lz_add(re, xmove<3>(re)); im = lz_add(im, xmove<3>(im)); }
+  if constexpr (LEVELS > 4) { re = lz_add(re, xmove<4>(re)); im = lz_add(im, xmove<4>(im)); }
+}
+
+// a lane's contribution l (a reduced v, doubled or not) placed in a coefficient: a real-part term
+// (l, 0) or an imaginary one (0, l); wrapped terms (index sum >= 6) carry xi = 9 + u:
+// (l, 0) -> (9l, l), (0, l) -> (-l, 9l) with -l from the negated reduced value nv
+__device__ __forceinline__ void place(const Lz& l, const Lz& nl, bool imag, bool wrap, Lz& re, Lz& im) {
+  if (!wrap) {
+    re = imag ? lz_zero() : l;
+    im = imag ? l : lz_zero();
+  } else {
+    const Lz l9 = lz_mul9(l);
+    re = imag ? nl : l9;
+    im = imag ? l9 : l;
+  }
+}
+
+// Per-lane roles of w_mul / w_sqr, fixed for the whole program (computed once, kept in registers:
+// the square-term table lookup was a per-operation vector load on the critical path).
+struct WLane {
+  // w_mul: output coefficient k, term i (operand b_jj), partial product q
+  uint8_t mk, mi, mjj, mq;
+  bool mwrap, mact;
+  // w_sqr: coefficient, pair {si, sj}, partial product q, flags
+  uint8_t sk, si, sj, sq;
+  bool slive, ssquare, sxi, sgrp;
+};
+__device__ __forceinline__ WLane wlane_init() {
+  WLane L{};
+  const int t = threadIdx.x;
+  {
+    const int grp = t >> 5, j = t & 31;
+    L.mact = grp < 6 && j < 24;
+    L.mk = grp < 6 ? grp : 0;
+    L.mi = L.mact ? j >> 2 : 0;
+    L.mq = j & 3;
+    int jj = (int)L.mk - (int)L.mi;
+    L.mwrap = jj < 0;
+    L.mjj = (uint8_t)(jj < 0 ? jj + 6 : jj);
+  }
+  {
+    const int grp = t >> 4, j = t & 15;
+    L.sgrp = grp < 6;
+    L.sk = L.sgrp ? grp : 0;
+    L.sq = j & 3;
+    const SqrTerm tm = c_sqr[L.sk][j >> 2];
+    L.slive = L.sgrp && tm.i >= 0;
+    L.si = L.slive ? tm.i : 0;
+    L.sj = L.slive ? tm.j : 0;
+    L.ssquare = L.si == L.sj;
+    L.sxi = L.slive && tm.xi;
+  }
+  return L;
+}
+
+// the lane pair (j = 0, 1) of a coefficient group reduces and stores re / im in parallel
+__device__ __forceinline__ void store_coeff(Fq2* __restrict__ dst, int k, int j, const Lz& re, const Lz& im) {
+  if (j < 2) {
+    const Fq v = lz_reduce(j ? im : re);
+    if (j) dst[k].c1 = v;
+    else dst[k].c0 = v;
+  }
+}
+
+// dst = a * b (dst distinct from a and b)
+SV_WG_FN void w_mul(const WLane& L, Fq2* __restrict__ dst, const Fq2* a, const Fq2* b) {
+  const int t = threadIdx.x;
+  if (t < 192) {  // waves 0-2 (uniform per wave)
+    const int q = L.mq;
+    // q: 0 a0 b0 (re +), 1 a1 b1 (re -), 2 a0 b1 (im +), 3 a1 b0 (im +)
+    const Fq ax = (q & 1) ? a[L.mi].c1 : a[L.mi].c0;
+    const Fq by = (q == 1 || q == 2) ? b[L.mjj].c1 : b[L.mjj].c0;
+    Fq v = ax * by;
+    if (!L.mact) v = Fq::zero();
+    const Fq nv = -v;
+    Lz re, im;
+    place(lz(q == 1 ? nv : v), lz(q == 1 ? v : nv), q >= 2, L.mwrap, re, im);
+    lane_sum<5>(re, im);
+    store_coeff(dst, L.mk, t & 31, re, im);
+  }
+  __syncthreads();
+}
+
+// dst = a^2 (dst distinct from a): coefficient k sums the pairs {i, j}, i + j = k (mod 6) of
+// c_sqr; a square term a_i^2 = a0^2 - a1^2 + 2 a0 a1 u, a cross term 2 a_i a_j
+SV_WG_FN void w_sqr(const WLane& L, Fq2* __restrict__ dst, const Fq2* a) {
+  const int t = threadIdx.x;
+  if (t < 128) {  // waves 0-1
+    const int q = L.sq;
+    const bool square = L.ssquare;
+    Fq x, y;
+    bool imag;
+    if (square) {  // a_i^2 = a0^2 - a1^2 + 2 a0 a1 u: q 0 a0 a0, 1 a1 a1 (re -), 2 a0 a1 (im x2)
+      x = (q & 1) ? a[L.si].c1 : a[L.si].c0;
+      y = q == 0 ? a[L.si].c0 : a[L.si].c1;
+      if (q == 2) x = a[L.si].c0;
+      imag = q == 2;
+    } else {
+      x = (q & 1) ? a[L.si].c1 : a[L.si].c0;
+      y = (q == 1 || q == 2) ? a[L.sj].c1 : a[L.sj].c0;
+      imag = q >= 2;
+    }
+    Fq v = x * y;
+    if (!L.slive || (square && q == 3)) v = Fq::zero();
+    const Fq nv = -v;
+    const bool neg = q == 1;
+    Lz l = lz(neg ? nv : v), nl = lz(neg ? v : nv);
+    if (!square || q == 2) {  // the pair counted twice / the 2 a0 a1 of a square
+      l = lz_add(l, l);
+      nl = lz_add(nl, nl);
+    }
+    Lz re, im;
+    place(l, nl, imag, L.sxi, re, im);
+    lane_sum<4>(re, im);
+    if (L.sgrp) store_coeff(dst, L.sk, t & 15, re, im);
+  }
+  __syncthreads();
+}
+
+// dst = frob^n(a): coefficient k -> conj^n(a_k) * gamma_(n,k)
+SV_WG_FN void w_frob(Fq2* __restrict__ dst, const Fq2* a, int n) {
+  const int t = threadIdx.x;
+  if (t < 64) {
+    const int k = t >> 2, q = t & 3;
+    const bool act = k < 6;
+    const int kk = act ? k : 0;
+    Fq2 x = a[kk];
+    if (n & 1) x.c1 = fq_neg2p(x.c1);
+    const uint32_t* g = c_gamma + ((n - 1) * 6 + kk) * 16;
+    Fq gc;
+#pragma unroll
+    for (int i = 0; i < 8; i++) gc.v[i] = g[(q == 1 || q == 2) ? 8 + i : i];
+    Fq v = ((q & 1) ? x.c1 : x.c0) * gc;
+    if (!act) v = Fq::zero();
+    const Fq nv = -v;
+    Lz re, im;
+    place(lz(q == 1 ? nv : v), lz(q == 1 ? v : nv), q >= 2, false, re, im);
+    lane_sum<2>(re, im);
+    if (act) store_coeff(dst, k, q, re, im);
+  }
+  __syncthreads();
+}
+
+// dst = conj(a) (odd w-coefficients negated) or a copy
+SV_WG_FN void w_conj(Fq2* __restrict__ dst, const Fq2* a, bool neg_odd = true) {
+  const int t = threadIdx.x;
+  if (t < 12) {
+    const int k = t >> 1;
+    const Fq v = (t & 1) ? a[k].c1 : a[k].c0;
+    const Fq r = (neg_odd && (k & 1)) ? fq_neg2p(v) : v;
+    if (t & 1) dst[k].c1 = r;
+    else dst[k].c0 = r;
+  }
+  __syncthreads();
+}
+
+// ni = N^-1 for N = a conj(a) (even coefficients = an Fq6 element c0 + c1 v + c2 v^2, v = w^2), as
+// in g_inv: the three t_j on three lanes, the norm d and its Fq2 inverse (one fe_inv) on one lane
+__device__ __forceinline__ void w_norm_inv(Fq2* __restrict__ ni, const Fq2* nn, Fq2* tj, Fq2* di) {
+  const int t = threadIdx.x;
+  if (t < 3) {
+    const Fq2 c0 = fq2_canon(nn[0]), c1 = fq2_canon(nn[2]), c2 = fq2_canon(nn[4]);
+    const Fq2 x = t == 0 ? c0 : (t == 1 ? c2 : c1);
+    const Fq2 y0 = t == 0 ? c1 : c0, y1 = t == 0 ? c2 : (t == 1 ? c1 : c2);
+    const Fq2 sq = x * x, pr = y0 * y1;
+    tj[t] = t == 0 ? sq - fq2_mul_xi(pr) : (t == 1 ? fq2_mul_xi(sq) - pr : sq - pr);
+  }
+  __syncthreads();
+  if (t == 0) {
+    const Fq2 d = fq2_canon(nn[0]) * tj[0] + fq2_mul_xi(fq2_canon(nn[4]) * tj[1] + fq2_canon(nn[2]) * tj[2]);
+    *di = fq2_inv(d);
+  }
+  __syncthreads();
+  if (t < 6) ni[t] = (t & 1) ? Fq2::zero() : tj[t >> 1] * (*di);
+  __syncthreads();
+}
+
+// ---- The decider as a straight-line program over LDS slots, run by one interpreter loop: each
+// operation's code exists once (no per-call register save / restore: an out-of-line operation cost
+// ~1500 cycles of call overhead, measured with tools/ubench_wg.hip), and the op stream is read with
+// wave-uniform scalar loads.  Operands: slot index, or a pair product D[i] / merged step M[i].
+enum WCode : uint8_t { OP_MUL, OP_SQR, OP_FROB, OP_CONJ, OP_COPY, OP_NORM_INV };
+struct WOp {
+  uint8_t code, imm;
+  uint16_t dst, a, b;
+};
+constexpr uint16_t kOpD = 1u << 14, kOpM = 2u << 14;
+enum WSlot {
+  S_F0, S_F1, S_FI, S_AC, S_NN, S_NI, S_TAB, S_X0 = S_TAB + 8, S_X1, S_FX, S_FX2, S_FX3, S_A, S_B, S_C, S_B6, S_B12,
+  S_B18, S_A6, S_A12, S_A18, S_A30, S_Y, S_Y36, S_L0, S_L1, S_L2, S_T0, S_T1, S_T2, S_E0, S_E1, S_E2, kSlots
+};
+constexpr int kMaxOps = 512;
+struct WProg {
+  WOp ops[kMaxOps];
+  int n;
+  constexpr void op(WCode c, int d, int a, int b = 0, int imm = 0) {
+    ops[n++] = WOp{(uint8_t)c, (uint8_t)imm, (uint16_t)d, (uint16_t)a, (uint16_t)b};
+  }
+  // dst = a^x, x = BN_X in width-4 NAF; table of odd powers a, a^3, a^5, a^7 and their conjugates
+  // (= inverses on the cyclotomic subgroup); the chain ping-pongs between S_X0 and S_X1
+  constexpr void pow_x(int dst, int a) {
+    const XNaf xn = make_xnaf();
+    op(OP_SQR, S_X0, a);
+    op(OP_COPY, S_TAB, a);
+    op(OP_CONJ, S_TAB + 4, a);
+    for (int e = 1; e < 4; e++) {
+      op(OP_MUL, S_TAB + e, S_TAB + e - 1, S_X0);
+      op(OP_CONJ, S_TAB + 4 + e, S_TAB + e);
+    }
+    auto tab = [](int d) { return S_TAB + (d > 0 ? (d - 1) / 2 : 4 + (-d - 1) / 2); };
+    int r = tab(xn.d[xn.len - 1]);
+    for (int i = xn.len - 2; i >= 0; i--) {
+      const int d = xn.d[i];
+      const bool last_sq = i == 0 && d == 0;
+      const int s1 = last_sq ? dst : (r == S_X0 ? S_X1 : S_X0);
+      op(OP_SQR, s1, r);
+      r = s1;
+      if (d) {
+        const int s2 = i == 0 ? dst : (r == S_X0 ? S_X1 : S_X0);
+        op(OP_MUL, s2, r, tab(d));
+        r = s2;
+      }
+    }
+  }
+};
+constexpr WProg make_wprog() {
+  WProg P{};
+  const MergeTab mt = make_merges();
+  (void)mt;
+  // Miller loop, merged step multipliers as in k_decide_lanes: f <- f^2 * (D_idx or M_m)
+  int m = 0, idx = 0;
+  for (int i = ATE_NAF_LEN - 1; i >= 1; i--) {
+    const int mul = ATE_NAF[i - 1] != 0 ? (kOpM | m++) : (kOpD | idx);
+    idx += ATE_NAF[i - 1] != 0 ? 2 : 1;
+    if (i == ATE_NAF_LEN - 1) {
+      P.op(OP_COPY, S_F0, mul);
+    } else {
+      P.op(OP_SQR, S_F1, S_F0);
+      P.op(OP_MUL, S_F0, S_F1, mul);
+    }
+  }
+  P.op(OP_MUL, S_F1, S_F0, kOpM | m);  // the two Frobenius steps
+  // final exponentiation (the chain of k_decide_lanes / curve.hpp final_exponentiation)
+  P.op(OP_CONJ, S_AC, S_F1);
+  P.op(OP_MUL, S_NN, S_F1, S_AC);
+  P.op(OP_NORM_INV, S_NI, S_NN);
+  P.op(OP_MUL, S_FI, S_AC, S_NI);        // f^-1
+  P.op(OP_MUL, S_B, S_AC, S_FI);         // easy part: f^(p^6 - 1)
+  P.op(OP_FROB, S_C, S_B, 0, 2);
+  P.op(OP_MUL, S_F0, S_C, S_B);          // ... ^(p^2 + 1) = K_F
+  P.pow_x(S_FX, S_F0);
+  P.op(OP_SQR, S_A, S_FX);
+  P.op(OP_MUL, S_B, S_A, S_FX);
+  P.op(OP_SQR, S_B6, S_B);
+  P.op(OP_SQR, S_B12, S_B6);
+  P.op(OP_MUL, S_B18, S_B12, S_B6);
+  P.pow_x(S_FX2, S_FX);
+  P.op(OP_SQR, S_A, S_FX2);
+  P.op(OP_MUL, S_B, S_A, S_FX2);
+  P.op(OP_SQR, S_A6, S_B);
+  P.op(OP_SQR, S_A12, S_A6);
+  P.op(OP_MUL, S_A18, S_A12, S_A6);
+  P.op(OP_MUL, S_A30, S_A18, S_A12);
+  P.pow_x(S_FX3, S_FX2);
+  P.op(OP_SQR, S_A, S_FX3);
+  P.op(OP_SQR, S_B, S_A);
+  P.op(OP_SQR, S_Y, S_B);                // fx3^8
+  P.op(OP_MUL, S_A, S_Y, S_FX3);
+  P.op(OP_SQR, S_B, S_A);
+  P.op(OP_SQR, S_Y36, S_B);              // fx3^36
+  P.op(OP_MUL, S_L2, S_F0, S_A6);        // l2 = f a6
+  P.op(OP_MUL, S_T0, S_Y36, S_A18);
+  P.op(OP_MUL, S_T1, S_T0, S_B12);
+  P.op(OP_CONJ, S_T2, S_T1);
+  P.op(OP_MUL, S_L1, S_T2, S_F0);        // l1 = conj(y36 a18 b12) f
+  P.op(OP_MUL, S_T0, S_Y36, S_A30);
+  P.op(OP_MUL, S_T1, S_T0, S_B18);
+  P.op(OP_SQR, S_T2, S_F0);
+  P.op(OP_MUL, S_T0, S_T1, S_T2);
+  P.op(OP_CONJ, S_L0, S_T0);             // l0 = conj(y36 a30 b18 f^2)
+  P.op(OP_FROB, S_T1, S_L1, 0, 1);
+  P.op(OP_MUL, S_E0, S_L0, S_T1);
+  P.op(OP_FROB, S_T2, S_L2, 0, 2);
+  P.op(OP_MUL, S_E1, S_E0, S_T2);
+  P.op(OP_FROB, S_T0, S_F0, 0, 3);
+  P.op(OP_MUL, S_E2, S_E1, S_T0);        // the result
+  return P;
+}
+__constant__ WProg c_wprog = make_wprog();
+constexpr int kResultSlot = S_E2;
+static_assert(make_wprog().n <= kMaxOps, "decider program too long");
+
+constexpr size_t kLdsE = 2 * (size_t)ATE_NUM_LINES * sizeof(LineCoeff);
+constexpr size_t kLdsD = (size_t)ATE_NUM_LINES * 6 * sizeof(Fq2);
+constexpr size_t kLdsSlots = (size_t)kSlots * 6 * sizeof(Fq2);
+constexpr size_t kLds = kLdsE + kLdsD + kLdsSlots;
+}  // namespace wg
+
+__global__ void __launch_bounds__(wg::kThreads) k_decide_wg(const G1Aff* __restrict__ lhs, const G1Aff* __restrict__ rhs,
+                                                          uint32_t n, const LineCoeff* __restrict__ L1,
+                                                          const LineCoeff* __restrict__ L2, int mont_in,
+                                                          int32_t* __restrict__ verdict, Fq12* __restrict__ gt) {
+  using namespace wg;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dec_lds[];
+  __shared__ Fq2 tj[3], di;
+  LineCoeff* E = reinterpret_cast<LineCoeff*>(dec_lds);
+  Fq2* D = reinterpret_cast<Fq2*>(dec_lds + kLdsE);
+  Fq2* S = reinterpret_cast<Fq2*>(dec_lds + kLdsE + kLdsD);
+  Fq2* M = reinterpret_cast<Fq2*>(E);  // the evaluated lines are dead once M is formed
+  const int t = threadIdx.x;
+  const uint32_t acc = blockIdx.x;
+  G1Aff p1 = load_aff_d(lhs, acc, mont_in), p2 = load_aff_d(rhs, acc, mont_in);
+  // prologue: lines at the accumulator's points, pair products D, merged step multipliers M
+  eval_lines(E, L1, L2, p1, p2, t, kThreads);
+  __syncthreads();
+  pair_products(D, E, t, kThreads);
+  __syncthreads();
+  merge_products(M, D, t, kThreads);
+  __syncthreads();
+  auto opnd = [&](uint16_t o) -> Fq2* {
+    const uint32_t i = o & (kOpD - 1);
+    return (o & kOpM) ? M + 6 * i : ((o & kOpD) ? D + 6 * i : S + 6 * i);
+  };
+  const WLane Ln = wlane_init();
+  const int nops = c_wprog.n;
+  for (int pc = 0; pc < nops; pc++) {
+    const WOp op = c_wprog.ops[pc];
+    Fq2* dst = S + 6 * op.dst;
+    const Fq2* a = opnd(op.a);
+    switch (op.code) {
+      case OP_MUL: w_mul(Ln, dst, a, opnd(op.b)); break;
+      case OP_SQR: w_sqr(Ln, dst, a); break;
+      case OP_FROB: w_frob(dst, a, op.imm); break;
+      case OP_CONJ: w_conj(dst, a, true); break;
+      case OP_COPY: w_conj(dst, a, false); break;
+      default: w_norm_inv(dst, a, tj, &di); break;
+    }
+  }
+  const Fq2* e = S + 6 * kResultSlot;
+  if (t < 6) {
+    if (t == 0) {
+      bool ok = fq2_canon(e[0]) == Fq2::one();
+      for (int k = 1; k < 6; k++) ok = ok && fq2_canon(e[k]).is_zero();
+      verdict[acc] = ok ? 1 : 0;
+    }
+    if (gt) reinterpret_cast<Fq2*>(gt + acc)[(t & 1) * 3 + (t >> 1)] = fq2_canon(e[t]);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Host side: prepared-line cache.  Each deciding key's lines live in their own immutable device
 // buffer, shared by refcount: a call holds its entry until its stream has synchronised, so a
@@ -682,13 +1150,32 @@ int decide_run_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const vo
   Fq12* d_gt = gt_host ? ws->carve<Fq12>(n) : nullptr;
   SV_HIP(hipEventRecord(ws->ev[0], st));
   // SVGPU_DECIDER_LANES = 48 (6 x 8 lanes per accumulator, 1 per wave; default) or 24 (6 x 4, 2 per wave)
-  static const int lanes = getenv("SVGPU_DECIDER_LANES") ? atoi(getenv("SVGPU_DECIDER_LANES")) : 48;
+  // SVGPU_DECIDER_LANES: 256 = k_decide_wg (one 4-wave block per accumulator: lowest latency, one
+  // block per CU), 48 / 24 = k_decide_lanes (one wave per accumulator, two blocks per CU: higher
+  // throughput once the accumulators outnumber the CUs).  Default: the workgroup kernel while every
+  // accumulator gets its own CU, the single-wave one beyond.
+  const int lanes_env = getenv("SVGPU_DECIDER_LANES") ? atoi(getenv("SVGPU_DECIDER_LANES")) : 0;
+  static thread_local int cu_dev = -1, cus = 256;
+  if (cu_dev != device) {
+    SV_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    cu_dev = device;
+  }
+  const int lanes = lanes_env ? lanes_env : (n <= (size_t)cus ? 256 : 48);
   static const int phases = getenv("SVGPU_DECIDER_PHASES") ? atoi(getenv("SVGPU_DECIDER_PHASES")) : 3;
   const G1Aff* dl = reinterpret_cast<const G1Aff*>(d_lhs);
   const G1Aff* dr = reinterpret_cast<const G1Aff*>(d_rhs);
   const int mont = form == SV_MONTGOMERY ? 1 : 0;
   const LineCoeff* L2 = lines + ATE_NUM_LINES;
-  if (lanes == 48)
+  static thread_local int wg_attr_dev = -1;  // > 64 KiB dynamic LDS opt-in, once per thread / device
+  if (lanes == 256 && wg_attr_dev != device) {
+    SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide_wg), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)wg::kLds));
+    wg_attr_dev = device;
+  }
+  if (lanes == 256)
+    hipLaunchKernelGGL(k_decide_wg, dim3((unsigned)n), dim3(wg::kThreads), wg::kLds, st, dl, dr, (uint32_t)n, lines,
+                       L2, mont, d_verdict, d_gt);
+  else if (lanes == 48)
     hipLaunchKernelGGL(k_decide_lanes<8>, dim3((unsigned)n), dim3(64), 0, st, dl, dr, (uint32_t)n, lines, L2, mont,
                        d_verdict, d_gt, phases);
   else

@@ -93,3 +93,28 @@ def test_aggregation_64_end_to_end(gpu):
     bad = svgpu.KzgAccumulator(b.g1_add(acc.lhs, b.G1_GEN), acc.rhs)
     with pytest.raises(svgpu.AssertionFailure):
         svgpu.KzgAs.decide(dk, bad)
+
+
+@pytest.mark.parametrize("lanes", ["256", "48", "24", "auto"])
+def test_both_decider_kernels_gt_and_first_fail(gpu, oracle_cpp, monkeypatch, lanes):
+    """k_decide_wg (one 4-wave block per accumulator) and k_decide_lanes (one wave per accumulator)
+    give the oracle's Gt values and first failure; 'auto' with more accumulators than CUs takes
+    the single-wave kernel for the whole batch."""
+    import svgpu
+    from svgpu import device as dv
+    from svgpu import encoding as enc
+    if lanes != "auto":
+        monkeypatch.setenv("SVGPU_DECIDER_LANES", lanes)
+    n = 300 if lanes == "auto" else 40
+    g2, sg2, accs = b.gen_decider_case(20, seed=0xBEEF, bad=[13])
+    accs = (accs * (n // 20 + 1))[:n]
+    accs[n - 3] = (None, None)                                  # identity pair: passes
+    L, R = enc.bases_array([a[0] for a in accs]), enc.bases_array([a[1] for a in accs])
+    ff, verdicts, gts = dv.decide(g2, sg2, _dev([a[0] for a in accs], gpu), _dev([a[1] for a in accs], gpu),
+                                  svgpu.SV_CANONICAL, want_gt=True)
+    eff, egt = oracle_cpp.decide_all(np.frombuffer(b.g2_bytes(g2), np.uint64), np.frombuffer(b.g2_bytes(sg2), np.uint64),
+                                     L, R, threads=0, want_gt=True)
+    assert ff == eff == 13
+    assert sum(1 for v in verdicts if not v) == n // 20 + (1 if n % 20 > 13 else 0)
+    for i in (0, 13, n - 3, n - 1):
+        assert [int(x) for x in gts[i]] == [enc.limbs_to_int(egt[i][4 * c:4 * c + 4]) for c in range(12)], i

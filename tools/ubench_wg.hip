@@ -1,0 +1,142 @@
+// Per-operation latency of the workgroup decider's Fq12 ops (csrc/decider.hip namespace wg) on one
+// 256-thread block: w_sqr / w_mul / w_frob in a dependent loop, timed with clock64 on the device.
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -Isnark-verifier-axiom_amd/csrc tools/ubench_wg.hip \
+//          snark-verifier-axiom_amd/csrc/runtime.cpp -o tools/ubench_wg
+#include "../snark-verifier-axiom_amd/csrc/decider.hip"
+
+#include <cstdio>
+
+using namespace sv;
+
+__global__ void __launch_bounds__(256) k_bench(int op, int iters, unsigned long long* cycles, uint32_t* sink) {
+  __shared__ Fq2 S[3 * 6];
+  const int t = threadIdx.x;
+  if (t < 6) {
+    S[t] = Fq2::one();
+    S[t].c1 = Fq::one();
+    S[6 + t] = S[t];
+  }
+  __syncthreads();
+  Fq2* a = S;
+  Fq2* b = S + 6;
+  Fq2* c = S + 12;
+  const wg::WLane L = wg::wlane_init();
+  const unsigned long long t0 = clock64();
+  for (int i = 0; i < iters; i++) {
+    if (op == 0) wg::w_sqr(L, c, a);
+    else if (op == 1) wg::w_mul(L, c, a, b);
+    else if (op == 2) wg::w_frob(c, a, 1);
+    else wg::w_conj(c, a);
+    Fq2* tmp = a;
+    a = c;
+    c = tmp;
+  }
+  const unsigned long long t1 = clock64();
+  if (t == 0) {
+    *cycles = t1 - t0;
+    sink[0] = a[0].c0.v[0];
+  }
+}
+
+// w_mul with parts switched off (mode bits): 1 no product, 2 no lane sum, 4 no lz_reduce,
+// 8 no barrier, 16 no LDS operand loads (registers instead)
+__device__ __noinline__ void w_mul_dbg(Fq2* __restrict__ dst, const Fq2* a, const Fq2* b, int mode) {
+  using namespace wg;
+  const int t = threadIdx.x, grp = t >> 5, j = t & 31;
+  if (grp < 6) {
+    const bool act = j < 24;
+    const int k = grp, i = act ? j >> 2 : 0, q = j & 3;
+    int jj = k - i;
+    const bool wrap = jj < 0;
+    if (wrap) jj += 6;
+    Fq ax, by;
+    if (mode & 16) {
+      ax = Fq::one();
+      ax.v[0] ^= t;
+      by = ax;
+    } else {
+      ax = (q & 1) ? a[i].c1 : a[i].c0;
+      by = (q == 1 || q == 2) ? b[jj].c1 : b[jj].c0;
+    }
+    Fq v = (mode & 1) ? ax : ax * by;
+    if (!act) v = Fq::zero();
+    const Fq nv = -v;
+    Lz re, im;
+    place(lz(q == 1 ? nv : v), lz(q == 1 ? v : nv), q >= 2, wrap, re, im);
+    if (!(mode & 2)) lane_sum<5>(re, im);
+    if (j == 0) {
+      if (mode & 4) {
+        Fq2 o;
+        for (int x = 0; x < 8; x++) o.c0.v[x] = re.v[x], o.c1.v[x] = im.v[x];
+        dst[k] = o;
+      } else {
+        dst[k] = {lz_reduce(re), lz_reduce(im)};
+      }
+    }
+  }
+  if (!(mode & 8)) __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_bench_dbg(int mode, int iters, unsigned long long* cycles, uint32_t* sink) {
+  __shared__ Fq2 S[3 * 6];
+  const int t = threadIdx.x;
+  if (t < 6) {
+    S[t] = Fq2::one();
+    S[6 + t] = S[t];
+  }
+  __syncthreads();
+  Fq2* a = S;
+  Fq2* b = S + 6;
+  Fq2* c = S + 12;
+  const unsigned long long t0 = clock64();
+  for (int i = 0; i < iters; i++) {
+    w_mul_dbg(c, a, b, mode);
+    Fq2* tmp = a;
+    a = c;
+    c = tmp;
+  }
+  const unsigned long long t1 = clock64();
+  if (t == 0) {
+    *cycles = t1 - t0;
+    sink[0] = a[0].c0.v[0];
+  }
+}
+
+__global__ void k_fqmul(int iters, unsigned long long* cycles, uint32_t* sink) {
+  Fq x = Fq::one();
+  x.v[0] ^= threadIdx.x;
+  const Fq y = x;
+  const unsigned long long t0 = clock64();
+  for (int i = 0; i < iters; i++) x = x * y;
+  const unsigned long long t1 = clock64();
+  if (threadIdx.x == 0) *cycles = t1 - t0;
+  sink[threadIdx.x] = x.v[0];
+}
+
+int main() {
+  unsigned long long* dc;
+  uint32_t* ds;
+  (void)hipMalloc(&dc, 8);
+  (void)hipMalloc(&ds, 4096);
+  const char* names[] = {"w_sqr", "w_mul", "w_frob", "w_conj"};
+  const int iters = 200;
+  for (int op = 0; op < 4; op++) {
+    hipLaunchKernelGGL(k_bench, dim3(1), dim3(256), 0, 0, op, 4, dc, ds);
+    hipLaunchKernelGGL(k_bench, dim3(1), dim3(256), 0, 0, op, iters, dc, ds);
+    unsigned long long c = 0;
+    (void)hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
+    printf("%-7s %8.1f cycles/op (clock64)\n", names[op], (double)c / iters);
+  }
+  for (int mode : {0, 1, 2, 4, 8, 16, 1 | 2 | 4, 1 | 2 | 4 | 8, 31}) {
+    hipLaunchKernelGGL(k_bench_dbg, dim3(1), dim3(256), 0, 0, mode, 4, dc, ds);
+    hipLaunchKernelGGL(k_bench_dbg, dim3(1), dim3(256), 0, 0, mode, iters, dc, ds);
+    unsigned long long c = 0;
+    (void)hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
+    printf("w_mul mode %2d %8.1f cycles/op\n", mode, (double)c / iters);
+  }
+  hipLaunchKernelGGL(k_fqmul, dim3(1), dim3(64), 0, 0, iters, dc, ds);
+  unsigned long long c = 0;
+  (void)hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
+  printf("%-7s %8.1f cycles/op (one wave, dependent Fq products)\n", "fq_mul", (double)c / iters);
+  return 0;
+}

@@ -10,6 +10,7 @@
 #include <exception>
 #include <mutex>
 #include <unordered_map>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -430,9 +431,24 @@ int sv_bn254_kzg_accumulate(const sv_g1_affine* lhs, const sv_g1_affine* rhs, si
   SV_TRY(sg.sync());
   SV_TRY(powers_device(sg.at(3), form, n, form, sg.at(2), sg.lease.get()->stream));
   SV_TRY(sg.sync());
-  Xyzz a, b;
-  SV_TRY(msm_run_device(sg.at(0), sg.at(2), n, form, dev, nullptr, &a));
-  SV_TRY(msm_run_device(sg.at(1), sg.at(2), n, form, dev, nullptr, &b));
+  // the lhs and rhs MSMs share the scalars and are independent: run them concurrently (each call
+  // leases its own stream + workspace), one on the caller and one on a pool worker
+  Xyzz ab[2];
+  int rc2[2] = {SV_OK, SV_OK};
+  std::string err2[2];
+  host_parallel_for(2, 1, [&](size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; k++) {
+      rc2[k] = msm_run_device(sg.at(k == 0 ? 0 : 1), sg.at(2), n, form, dev, nullptr, &ab[k]);
+      if (rc2[k] != SV_OK) err2[k] = sv::last_error();
+    }
+  });
+  for (int k = 0; k < 2; k++)
+    if (rc2[k] != SV_OK) {
+      sv::set_error("%s", err2[k].c_str());
+      return rc2[k];
+    }
+  const Xyzz& a = ab[0];
+  const Xyzz& b = ab[1];
   affine_out(a, form, out_lhs);
   affine_out(b, form, out_rhs);
   return SV_OK;

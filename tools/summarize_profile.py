@@ -3,7 +3,7 @@
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  gfx950 correction (MI355X_MICROARCH.md, HBM):
 FETCH_SIZE reads exactly half the bytes of wide (16 B/lane) coalesced streaming reads; other access
 widths are uncalibrated, so both the raw and the x2-corrected read figures are recorded.
-usage: python3 tools/summarize_profile.py gpurun_out/prof profiles r01
+usage: python3 tools/summarize_profile.py gpurun_out/prof profiles r02
 """
 import csv
 import json
@@ -47,13 +47,34 @@ for k in sorted(pmc["FETCH_SIZE"], key=lambda k: -pmc["FETCH_SIZE"][k]):
     f = pmc["FETCH_SIZE"][k]
     w = pmc["WRITE_SIZE"].get(k, 0.0)
     lines.append("| %s | %.0f | %.1f | %.0f | %.1f |" % (k, f, 2 * f * 1024 / 1e6, w, (2 * f + w) * 1024 / 1e6))
+# FETCH_SIZE calibration (tools/calib_fetch.hip): known bytes / FETCH_SIZE bytes per kernel dispatch
+calib = {}
+cal_csv = os.path.join(src, "pmc_calib", "run_counter_collection.csv")
+if os.path.exists(cal_csv):
+    known = {"gather64_64MiB": 1048576 * 16 * 64, "gather64_1GiB": 1048576 * 16 * 64, "stream16": 256 << 20}
+    rows_c = [r for r in csv.DictReader(open(cal_csv)) if short(r["Kernel_Name"]) in ("k_gather64", "k_stream")]
+    rows_c.sort(key=lambda r: int(r["Dispatch_Id"]))
+    names = [n for n, r in zip(("gather64_64MiB", "gather64_1GiB"), [r for r in rows_c if short(r["Kernel_Name"]) == "k_gather64"])]
+    names += ["stream16"] if any(short(r["Kernel_Name"]) == "k_stream" for r in rows_c) else []
+    for name, r in zip(names, rows_c):
+        v = float(r["Counter_Value"])
+        calib[name] = {"fetch_kib": v, "known_bytes": known[name], "factor": known[name] / (v * 1024) if v else None}
+    lines += ["", "## FETCH_SIZE calibration (tools/calib_fetch.hip, known byte counts)", "",
+              "| pattern | FETCH_SIZE KiB | known MB | factor (known / FETCH_SIZE) |", "|---|---|---|---|"]
+    for k, v in calib.items():
+        lines.append("| %s | %.0f | %.1f | %.3f |" % (k, v["fetch_kib"], v["known_bytes"] / 1e6, v["factor"] or 0))
 open(os.path.join(dst, f"{tag}_kernel_stats.md"), "w").write("\n".join(lines) + "\n")
 acc_f = pmc["FETCH_SIZE"].get("k_accumulate")
 acc_w = pmc["WRITE_SIZE"].get("k_accumulate")
 if acc_f is not None:
+    g = calib.get("gather64_64MiB", {}).get("factor")
+    factor = g if g else 2.0
     json.dump({"kernel": "k_accumulate", "source": f"profiles/{tag}_kernel_stats.md",
-               "fetch_kib_raw": acc_f, "write_kib": acc_w,
-               "hbm_bytes_per_launch": (2 * acc_f + (acc_w or 0)) * 1024,
-               "correction": "reads doubled per MI355X_MICROARCH.md HBM note (uncalibrated for 16-B gathers)"},
+               "fetch_kib_raw": acc_f, "write_kib": acc_w, "read_factor": factor,
+               "hbm_bytes_per_launch": (factor * acc_f + (acc_w or 0)) * 1024,
+               "correction": "reads scaled by the factor calibrated on k_accumulate's own access pattern "
+                             "(random 64-B gathers from a 64 MiB table, tools/calib_fetch.hip) -- the "
+                             "MI355X_MICROARCH.md HBM note calibrates only 16-B streaming reads (x2)"
+                             if g else "reads doubled per MI355X_MICROARCH.md HBM note (calibration missing)"},
               open(os.path.join(dst, "pmc_accumulate.json"), "w"), indent=1)
 print("\n".join(lines))

@@ -302,21 +302,28 @@ def main():
         }
         del hB, hS, refs
 
-    # ---- KZG decider (config 3): accumulators per GPU, timed the same way
+    # ---- KZG decider (config 3): accumulators per GPU (N > 1: rank r holds global accumulators
+    #      [r dn, (r + 1) dn) and the first failing global index comes from one MIN all-reduce)
     dn = args.decider_n
     g2, sg2, accs = ob.gen_decider_case(16, seed=ob.SEED_TRAPDOOR)
     accs = (accs * ((dn + 15) // 16))[:dn]
     from svgpu import encoding as enc
     L = torch.from_numpy(enc.bases_array([a[0] for a in accs]).view(np.int64)).to(dev)
     R = torch.from_numpy(enc.bases_array([a[1] for a in accs]).view(np.int64)).to(dev)
-    ff, _, _ = dv.decide(g2, sg2, L, R)
+
+    def decide_step():
+        if world > 1:
+            return parallel.sharded_decide_device(g2, sg2, L, R, rank * dn, svgpu.SV_CANONICAL)
+        ff_, _, _ = dv.decide(g2, sg2, L, R)
+        return ff_
+    ff = decide_step()
     dsteps = max(1, args.steps // 2)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     dec_kernel_ms = []
     for _ in range(dsteps):
-        ff, _, _ = dv.decide(g2, sg2, L, R)
+        ff = decide_step()
         dec_kernel_ms.append(dv.last_decide_kernel_ms())
     torch.cuda.synchronize()
     barrier()

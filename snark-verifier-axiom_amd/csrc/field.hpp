@@ -8,7 +8,7 @@
 // Montgomery multiplication on the device is finely-integrated product scanning over 32-bit limbs:
 // every partial product is one v_mad_u64_u32 (32x32+64 -> 64, ~30 per clock per CU, measured
 // 18.2 T/s chip-wide by tools/ubench_fpmul.hip) whose carry-out feeds a v_addc -- 128 products,
-// 130 G mul/s (tools/ubench_mulvar).  The host build of the same templates uses portable CIOS.
+// 130 G mul/s (round-1 variable-operand microbenchmark; its binary was dropped from the tree).  The host build of the same templates uses portable CIOS.
 // Elements are kept fully reduced in [0, p) so equality is bitwise.
 #pragma once
 #include <cstdint>
@@ -225,12 +225,13 @@ SV_HD Fe<M> fe_dbl(const Fe<M>& a) {
 #if defined(__HIP_DEVICE_COMPILE__)
 // acc (64 bit) += a * b with the carry out of v_mad_u64_u32 collected in ovf: two VALU
 // instructions per partial product and no re-packing of 64-bit addends (the compiler's CIOS
-// lowering spends ~2.3 v_mov per product on that; tools/ubench_mulvar: 99.6 -> 130 G mul/s).
+// lowering spends ~2.3 v_mov per product on that; round-1 microbenchmark: 99.6 -> 130 G mul/s).
 // VCC hazard: the v_addc reads VCC right after the quarter-rate v_mad_u64_u32 wrote it; the mad's
 // multi-pass issue occupies the wave's VALU past the 2-state VALU-SGPR-write window, so no s_nop is
 // needed inside a block (every result is checked bit-exact against the oracle in tests/).  hipcc
 // pads one state after each asm block, so products are issued four per block (single-wave latency
-// 737 -> 607 ns per multiply, tools/ubench_mulgroup).
+// 737 -> 607 ns per multiply, round-1 microbenchmark; tools/ubench_wg.hip measures the
+// current per-product latency: 1517 cycles per dependent product on one wave).
 #define SV_MAC_STEP(A, B) "v_mad_u64_u32 %0, vcc, " A ", " B ", %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"
 __device__ __forceinline__ void mac_carry(uint64_t& acc, uint32_t& ovf, uint32_t a, uint32_t b) {
   asm(SV_MAC_STEP("%2", "%3") : "+v"(acc), "+v"(ovf) : "v"(a), "v"(b) : "vcc");

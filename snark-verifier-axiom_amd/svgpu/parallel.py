@@ -82,3 +82,15 @@ def combine_first_fail(local_first_fail: int, shard_offset: int, group=None) -> 
     dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
     g = int(t.item())
     return -1 if g == world_sentinel else g
+
+
+def sharded_decide_device(g2, s_g2, lhs: torch.Tensor, rhs: torch.Tensor, shard_offset: int, form: int,
+                          group=None) -> int:
+    """decide_all over accumulator shards: this rank decides its HBM-resident shard (global indices
+    [shard_offset, shard_offset + len)) and the first failing GLOBAL index (-1: all pass) comes
+    from one MIN all-reduce, as the reference's sequential try_collect would report it
+    (decider.rs:70-80)."""
+    from .device import decide
+
+    local, _, _ = decide(g2, s_g2, lhs, rhs, form)
+    return combine_first_fail(local, shard_offset, group)

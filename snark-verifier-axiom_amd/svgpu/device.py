@@ -59,8 +59,19 @@ def msm_partial(bases: torch.Tensor, scalars: torch.Tensor, form: int = _lib.SV_
 
 
 def msm(bases: torch.Tensor, scalars: torch.Tensor, form: int = _lib.SV_MONTGOMERY):
-    from .loader import fold_partials
-    return fold_partials([msm_partial(bases, scalars, form)])
+    """One device's MSM -> affine point (canonical ints; None = identity).  The Jacobian partial
+    goes straight from sv_bn254_g1_msm_device into sv_bn254_g1_fold (no Python-int round trip)."""
+    if bases.shape[0] != scalars.shape[0]:
+        raise ValueError("bases and scalars differ in length")
+    d = _dev_index(bases)
+    part = _lib.sv_g1_jacobian()
+    _lib.check(_lib.lib.sv_bn254_g1_msm_device(bases.data_ptr(), scalars.data_ptr(), bases.shape[0], form, d,
+                                               _stream_handle(bases.device), ctypes.byref(part)),
+               "sv_bn254_g1_msm_device")
+    out = _lib.sv_g1_affine()
+    _lib.check(_lib.lib.sv_bn254_g1_fold(ctypes.byref(part), 1, ctypes.byref(out), _lib.SV_CANONICAL),
+               "sv_bn254_g1_fold")
+    return enc.g1_from_struct(out)
 
 
 def last_msm_stats() -> dict:

@@ -588,7 +588,23 @@ __device__ __forceinline__ uint32_t xmove(uint32_t x) {
   else if constexpr (L == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // lane ^ 2
   else if constexpr (L == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // 7 - i in 8
   else if constexpr (L == 3) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);  // 15 - i in 16
+  else if constexpr (L == 5) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x124, 0xF, 0xF, false);  // row_ror 4
+  else if constexpr (L == 6) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, false);  // row_ror 8
   else return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);  // lane ^ 16 (bit mode, within 32)
+}
+// 16-B LDS accesses of a 32-B field element (slots, D, M and the gamma table are 32-B aligned)
+__device__ __forceinline__ Fq ld_fq(const Fq* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  const uint4 x = q[0], y = q[1];
+  Fq r;
+  r.v[0] = x.x, r.v[1] = x.y, r.v[2] = x.z, r.v[3] = x.w;
+  r.v[4] = y.x, r.v[5] = y.y, r.v[6] = y.z, r.v[7] = y.w;
+  return r;
+}
+__device__ __forceinline__ void st_fq(Fq* p, const Fq& v) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = make_uint4(v.v[0], v.v[1], v.v[2], v.v[3]);
+  q[1] = make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]);
 }
 // Lazily reduced sums: a lane's contribution and the cross-lane partial sums are plain 9-limb
 // integers (every sum here stays below 300 p < 2^263), reduced mod p ONCE per coefficient -- a
@@ -629,7 +645,10 @@ __device__ __forceinline__ Lz lz_mul9(const Lz& a) {  // (a << 3) + a
 // the Montgomery product is exact for inputs below 2p (4 p^2 < 2^256 p) and returns them reduced.
 __device__ __forceinline__ Fq lz_reduce(const Lz& a) {
   const uint64_t hi = ((uint64_t)a.v[8] << 32) | a.v[7];  // a >> 224
-  const uint32_t k = (uint32_t)((double)hi / (double)(FQ_P[7] + 1ull));
+  // times 1 / (p_top + 1) instead of a division: the product stays below a / p (the divisor's
+  // rounding up outweighs the multiply's rounding error), so k is still floor(a / p) or one less
+  constexpr double kInvPtop = 1.0 / (double)(FQ_P[7] + 1ull);
+  const uint32_t k = (uint32_t)((double)hi * kInvPtop);
   uint32_t r[9];
   uint32_t br = 0;
   uint64_t carry = 0;
@@ -670,15 +689,27 @@ __device__ __forceinline__ Lz xmove(const Lz& a) {
   for (int i = 0; i < 9; i++) r.v[i] = xmove<L>(a.v[i]);
   return r;
 }
-// (re, im) summed over aligned groups of 2^LEVELS lanes; every lane of a group ends with the sum
-// (after levels 0 and 1 a quad is uniform, so the mirrors of levels 2 and 3 reach the other half)
+// (re, im) summed over aligned groups of 2^LEVELS lanes as a reduce-scatter: the first level
+// trades halves with the neighbour lane, so even lanes carry re and odd lanes im from then on and
+// every later level moves and adds ONE 9-limb value (not two).  The later levels pair lanes of
+// equal parity: lane ^ 2, then row rotations by 4 and 8 (within a 16-lane row), then lane ^ 16.
+// Every even (odd) lane of a group ends with the group's re (im) sum.
 template <int LEVELS>
-__device__ __forceinline__ void lane_sum(Lz& re, Lz& im) {
-  if constexpr (LEVELS > 0) { re = lz_add(re, xmove<0>(re)); im = lz_add(im, xmove<0>(im)); }
-  if constexpr (LEVELS > 1) { re = lz_add(re, xmove<1>(re)); im = lz_add(im, xmove<1>(im)); }
-  if constexpr (LEVELS > 2) { re = lz_add(re, xmove<2>(re)); im = lz_add(im, xmove<2>(im)); }
-  if constexpr (LEVELS > 3) { re = lz_add(re, xmove<3>(re)); im = lz_add(im, xmove<3>(im)); }
-  if constexpr (LEVELS > 4) { re = lz_add(re, xmove<4>(re)); im = lz_add(im, xmove<4>(im)); }
+__device__ __forceinline__ Lz lane_sum(const Lz& re, const Lz& im) {
+  static_assert(LEVELS == 1 || LEVELS == 2 || LEVELS == 4 || LEVELS == 5, "row rotations need 16-lane groups");
+  const bool odd = threadIdx.x & 1;
+  Lz keep, send;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    keep.v[i] = odd ? im.v[i] : re.v[i];
+    send.v[i] = odd ? re.v[i] : im.v[i];
+  }
+  Lz v = lz_add(keep, xmove<0>(send));
+  if constexpr (LEVELS > 1) v = lz_add(v, xmove<1>(v));
+  if constexpr (LEVELS > 2) v = lz_add(v, xmove<5>(v));
+  if constexpr (LEVELS > 3) v = lz_add(v, xmove<6>(v));
+  if constexpr (LEVELS > 4) v = lz_add(v, xmove<4>(v));
+  return v;
 }
 
 // a lane's contribution l (a reduced v, doubled or not) placed in a coefficient: a real-part term
@@ -734,12 +765,8 @@ __device__ __forceinline__ WLane wlane_init() {
 }
 
 // the lane pair (j = 0, 1) of a coefficient group reduces and stores re / im in parallel
-__device__ __forceinline__ void store_coeff(Fq2* __restrict__ dst, int k, int j, const Lz& re, const Lz& im) {
-  if (j < 2) {
-    const Fq v = lz_reduce(j ? im : re);
-    if (j) dst[k].c1 = v;
-    else dst[k].c0 = v;
-  }
+__device__ __forceinline__ void store_coeff(Fq2* __restrict__ dst, int k, int j, const Lz& v) {
+  if (j < 2) st_fq(j ? &dst[k].c1 : &dst[k].c0, lz_reduce(v));
 }
 
 // dst = a * b (dst distinct from a and b)
@@ -748,15 +775,14 @@ SV_WG_FN void w_mul(const WLane& L, Fq2* __restrict__ dst, const Fq2* a, const F
   if (t < 192) {  // waves 0-2 (uniform per wave)
     const int q = L.mq;
     // q: 0 a0 b0 (re +), 1 a1 b1 (re -), 2 a0 b1 (im +), 3 a1 b0 (im +)
-    const Fq ax = (q & 1) ? a[L.mi].c1 : a[L.mi].c0;
-    const Fq by = (q == 1 || q == 2) ? b[L.mjj].c1 : b[L.mjj].c0;
+    const Fq ax = ld_fq((q & 1) ? &a[L.mi].c1 : &a[L.mi].c0);
+    const Fq by = ld_fq((q == 1 || q == 2) ? &b[L.mjj].c1 : &b[L.mjj].c0);
     Fq v = ax * by;
     if (!L.mact) v = Fq::zero();
-    const Fq nv = -v;
+    const Fq nv = fq_neg2p(v);
     Lz re, im;
     place(lz(q == 1 ? nv : v), lz(q == 1 ? v : nv), q >= 2, L.mwrap, re, im);
-    lane_sum<5>(re, im);
-    store_coeff(dst, L.mk, t & 31, re, im);
+    store_coeff(dst, L.mk, t & 31, lane_sum<5>(re, im));
   }
   __syncthreads();
 }
@@ -768,21 +794,16 @@ SV_WG_FN void w_sqr(const WLane& L, Fq2* __restrict__ dst, const Fq2* a) {
   if (t < 128) {  // waves 0-1
     const int q = L.sq;
     const bool square = L.ssquare;
-    Fq x, y;
-    bool imag;
-    if (square) {  // a_i^2 = a0^2 - a1^2 + 2 a0 a1 u: q 0 a0 a0, 1 a1 a1 (re -), 2 a0 a1 (im x2)
-      x = (q & 1) ? a[L.si].c1 : a[L.si].c0;
-      y = q == 0 ? a[L.si].c0 : a[L.si].c1;
-      if (q == 2) x = a[L.si].c0;
-      imag = q == 2;
-    } else {
-      x = (q & 1) ? a[L.si].c1 : a[L.si].c0;
-      y = (q == 1 || q == 2) ? a[L.sj].c1 : a[L.sj].c0;
-      imag = q >= 2;
-    }
+    // a_i^2 = a0^2 - a1^2 + 2 a0 a1 u: q 0 a0 a0, 1 a1 a1 (re -), 2 a0 a1 (im x2); a cross term
+    // takes x from a_i (q odd: c1) and y from a_j (q 1, 2: c1)
+    const bool xc1 = square ? q == 1 : (q & 1);
+    const bool yc1 = square ? q != 0 : (q == 1 || q == 2);
+    const bool imag = square ? q == 2 : q >= 2;
+    const Fq x = ld_fq(xc1 ? &a[L.si].c1 : &a[L.si].c0);
+    const Fq y = ld_fq(yc1 ? &a[L.sj].c1 : &a[L.sj].c0);
     Fq v = x * y;
     if (!L.slive || (square && q == 3)) v = Fq::zero();
-    const Fq nv = -v;
+    const Fq nv = fq_neg2p(v);
     const bool neg = q == 1;
     Lz l = lz(neg ? nv : v), nl = lz(neg ? v : nv);
     if (!square || q == 2) {  // the pair counted twice / the 2 a0 a1 of a square
@@ -791,32 +812,29 @@ SV_WG_FN void w_sqr(const WLane& L, Fq2* __restrict__ dst, const Fq2* a) {
     }
     Lz re, im;
     place(l, nl, imag, L.sxi, re, im);
-    lane_sum<4>(re, im);
-    if (L.sgrp) store_coeff(dst, L.sk, t & 15, re, im);
+    const Lz s = lane_sum<4>(re, im);
+    if (L.sgrp) store_coeff(dst, L.sk, t & 15, s);
   }
   __syncthreads();
 }
 
-// dst = frob^n(a): coefficient k -> conj^n(a_k) * gamma_(n,k)
-SV_WG_FN void w_frob(Fq2* __restrict__ dst, const Fq2* a, int n) {
+// dst = frob^n(a): coefficient k -> conj^n(a_k) * gamma_(n,k); gam = c_gamma staged in LDS
+SV_WG_FN void w_frob(Fq2* __restrict__ dst, const Fq2* a, int n, const Fq* gam) {
   const int t = threadIdx.x;
   if (t < 64) {
     const int k = t >> 2, q = t & 3;
     const bool act = k < 6;
     const int kk = act ? k : 0;
-    Fq2 x = a[kk];
-    if (n & 1) x.c1 = fq_neg2p(x.c1);
-    const uint32_t* g = c_gamma + ((n - 1) * 6 + kk) * 16;
-    Fq gc;
-#pragma unroll
-    for (int i = 0; i < 8; i++) gc.v[i] = g[(q == 1 || q == 2) ? 8 + i : i];
-    Fq v = ((q & 1) ? x.c1 : x.c0) * gc;
+    Fq x = ld_fq((q & 1) ? &a[kk].c1 : &a[kk].c0);
+    if ((n & 1) && (q & 1)) x = fq_neg2p(x);
+    const Fq gc = ld_fq(gam + ((n - 1) * 6 + kk) * 2 + ((q == 1 || q == 2) ? 1 : 0));
+    Fq v = x * gc;
     if (!act) v = Fq::zero();
-    const Fq nv = -v;
+    const Fq nv = fq_neg2p(v);
     Lz re, im;
     place(lz(q == 1 ? nv : v), lz(q == 1 ? v : nv), q >= 2, false, re, im);
-    lane_sum<2>(re, im);
-    if (act) store_coeff(dst, k, q, re, im);
+    const Lz s = lane_sum<2>(re, im);
+    if (act) store_coeff(dst, k, q, s);
   }
   __syncthreads();
 }
@@ -973,7 +991,8 @@ static_assert(make_wprog().n <= kMaxOps, "decider program too long");
 constexpr size_t kLdsE = 2 * (size_t)ATE_NUM_LINES * sizeof(LineCoeff);
 constexpr size_t kLdsD = (size_t)ATE_NUM_LINES * 6 * sizeof(Fq2);
 constexpr size_t kLdsSlots = (size_t)kSlots * 6 * sizeof(Fq2);
-constexpr size_t kLds = kLdsE + kLdsD + kLdsSlots;
+constexpr size_t kLdsGamma = sizeof(c_gamma);
+constexpr size_t kLds = kLdsE + kLdsD + kLdsSlots + kLdsGamma;
 }  // namespace wg
 
 __global__ void __launch_bounds__(wg::kThreads) k_decide_wg(const G1Aff* __restrict__ lhs, const G1Aff* __restrict__ rhs,
@@ -987,7 +1006,9 @@ __global__ void __launch_bounds__(wg::kThreads) k_decide_wg(const G1Aff* __restr
   Fq2* D = reinterpret_cast<Fq2*>(dec_lds + kLdsE);
   Fq2* S = reinterpret_cast<Fq2*>(dec_lds + kLdsE + kLdsD);
   Fq2* M = reinterpret_cast<Fq2*>(E);  // the evaluated lines are dead once M is formed
+  Fq* gam = reinterpret_cast<Fq*>(dec_lds + kLdsE + kLdsD + kLdsSlots);
   const int t = threadIdx.x;
+  for (int i = t; i < (int)(kLdsGamma / 4); i += kThreads) reinterpret_cast<uint32_t*>(gam)[i] = c_gamma[i];
   const uint32_t acc = blockIdx.x;
   G1Aff p1 = load_aff_d(lhs, acc, mont_in), p2 = load_aff_d(rhs, acc, mont_in);
   // prologue: lines at the accumulator's points, pair products D, merged step multipliers M
@@ -1003,14 +1024,16 @@ __global__ void __launch_bounds__(wg::kThreads) k_decide_wg(const G1Aff* __restr
   };
   const WLane Ln = wlane_init();
   const int nops = c_wprog.n;
+  WOp nxt = c_wprog.ops[0];
   for (int pc = 0; pc < nops; pc++) {
-    const WOp op = c_wprog.ops[pc];
+    const WOp op = nxt;
+    if (pc + 1 < nops) nxt = c_wprog.ops[pc + 1];  // next op's scalar load in flight during this one
     Fq2* dst = S + 6 * op.dst;
     const Fq2* a = opnd(op.a);
     switch (op.code) {
       case OP_MUL: w_mul(Ln, dst, a, opnd(op.b)); break;
       case OP_SQR: w_sqr(Ln, dst, a); break;
-      case OP_FROB: w_frob(dst, a, op.imm); break;
+      case OP_FROB: w_frob(dst, a, op.imm, gam); break;
       case OP_CONJ: w_conj(dst, a, true); break;
       case OP_COPY: w_conj(dst, a, false); break;
       default: w_norm_inv(dst, a, tj, &di); break;

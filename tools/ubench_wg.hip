@@ -10,12 +10,14 @@ using namespace sv;
 
 __global__ void __launch_bounds__(256) k_bench(int op, int iters, unsigned long long* cycles, uint32_t* sink) {
   __shared__ Fq2 S[3 * 6];
+  __shared__ Fq gam[3 * 6 * 2];
   const int t = threadIdx.x;
   if (t < 6) {
     S[t] = Fq2::one();
     S[t].c1 = Fq::one();
     S[6 + t] = S[t];
   }
+  for (int i = t; i < 3 * 6 * 16; i += 256) reinterpret_cast<uint32_t*>(gam)[i] = c_gamma[i];
   __syncthreads();
   Fq2* a = S;
   Fq2* b = S + 6;
@@ -25,7 +27,7 @@ __global__ void __launch_bounds__(256) k_bench(int op, int iters, unsigned long 
   for (int i = 0; i < iters; i++) {
     if (op == 0) wg::w_sqr(L, c, a);
     else if (op == 1) wg::w_mul(L, c, a, b);
-    else if (op == 2) wg::w_frob(c, a, 1);
+    else if (op == 2) wg::w_frob(c, a, 1, gam);
     else wg::w_conj(c, a);
     Fq2* tmp = a;
     a = c;
@@ -63,7 +65,7 @@ __device__ __noinline__ void w_mul_dbg(Fq2* __restrict__ dst, const Fq2* a, cons
     const Fq nv = -v;
     Lz re, im;
     place(lz(q == 1 ? nv : v), lz(q == 1 ? v : nv), q >= 2, wrap, re, im);
-    if (!(mode & 2)) lane_sum<5>(re, im);
+    if (!(mode & 2)) re = lane_sum<5>(re, im);
     if (j == 0) {
       if (mode & 4) {
         Fq2 o;

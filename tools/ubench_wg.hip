@@ -5,6 +5,7 @@
 #include "../snark-verifier-axiom_amd/csrc/decider.hip"
 
 #include <cstdio>
+#include <vector>
 
 using namespace sv;
 
@@ -41,39 +42,37 @@ __global__ void __launch_bounds__(256) k_bench(int op, int iters, unsigned long 
 }
 
 // w_mul with parts switched off (mode bits): 1 no product, 2 no lane sum, 4 no lz_reduce,
-// 8 no barrier, 16 no LDS operand loads (registers instead)
-__device__ __noinline__ void w_mul_dbg(Fq2* __restrict__ dst, const Fq2* a, const Fq2* b, int mode) {
+// 8 no barrier, 16 no LDS operand loads (registers instead); the same code as wg::w_mul otherwise
+__device__ __forceinline__ void w_mul_dbg(const wg::WLane& L, Fq2* __restrict__ dst, const Fq2* a, const Fq2* b,
+                                          int mode) {
   using namespace wg;
-  const int t = threadIdx.x, grp = t >> 5, j = t & 31;
-  if (grp < 6) {
-    const bool act = j < 24;
-    const int k = grp, i = act ? j >> 2 : 0, q = j & 3;
-    int jj = k - i;
-    const bool wrap = jj < 0;
-    if (wrap) jj += 6;
+  const int t = threadIdx.x;
+  if (t < 192) {
+    const int q = L.mq;
     Fq ax, by;
     if (mode & 16) {
       ax = Fq::one();
       ax.v[0] ^= t;
       by = ax;
     } else {
-      ax = (q & 1) ? a[i].c1 : a[i].c0;
-      by = (q == 1 || q == 2) ? b[jj].c1 : b[jj].c0;
+      ax = ld_fq((q & 1) ? &a[L.mi].c1 : &a[L.mi].c0);
+      by = ld_fq((q == 1 || q == 2) ? &b[L.mjj].c1 : &b[L.mjj].c0);
     }
     Fq v = (mode & 1) ? ax : ax * by;
-    if (!act) v = Fq::zero();
-    const Fq nv = -v;
+    if (!L.mact) v = Fq::zero();
+    const Fq nv = fq_neg2p(v);
     Lz re, im;
-    place(lz(q == 1 ? nv : v), lz(q == 1 ? v : nv), q >= 2, wrap, re, im);
-    if (!(mode & 2)) re = lane_sum<5>(re, im);
-    if (j == 0) {
+    place(lz(q == 1 ? nv : v), lz(q == 1 ? v : nv), q >= 2, L.mwrap, re, im);
+    const Lz s = (mode & 2) ? re : lane_sum<5>(re, im);
+    const int j = t & 31;
+    if (j < 2) {
+      Fq r;
       if (mode & 4) {
-        Fq2 o;
-        for (int x = 0; x < 8; x++) o.c0.v[x] = re.v[x], o.c1.v[x] = im.v[x];
-        dst[k] = o;
+        for (int x = 0; x < 8; x++) r.v[x] = s.v[x];
       } else {
-        dst[k] = {lz_reduce(re), lz_reduce(im)};
+        r = lz_reduce(s);
       }
+      st_fq(j ? &dst[L.mk].c1 : &dst[L.mk].c0, r);
     }
   }
   if (!(mode & 8)) __syncthreads();
@@ -90,9 +89,10 @@ __global__ void __launch_bounds__(256) k_bench_dbg(int mode, int iters, unsigned
   Fq2* a = S;
   Fq2* b = S + 6;
   Fq2* c = S + 12;
+  const wg::WLane L = wg::wlane_init();
   const unsigned long long t0 = clock64();
   for (int i = 0; i < iters; i++) {
-    w_mul_dbg(c, a, b, mode);
+    w_mul_dbg(L, c, a, b, mode);
     Fq2* tmp = a;
     a = c;
     c = tmp;
@@ -115,6 +115,45 @@ __global__ void k_fqmul(int iters, unsigned long long* cycles, uint32_t* sink) {
   sink[threadIdx.x] = x.v[0];
 }
 
+// one lane inverting in Fq2 (the decider's w_norm_inv), dependent chain
+__global__ void k_inv(int iters, unsigned long long* cycles, uint32_t* sink) {
+  Fq2 x = Fq2::one();
+  x.c1 = Fq::one();
+  x.c0.v[0] ^= threadIdx.x;
+  const unsigned long long t0 = clock64();
+  for (int i = 0; i < iters; i++) x = fq2_inv(x);
+  const unsigned long long t1 = clock64();
+  if (threadIdx.x == 0) *cycles = t1 - t0;
+  sink[threadIdx.x] = x.c0.v[0];
+}
+
+// every CU busy (grid = CU count) with the w_sqr loop: shader clock = d(memtime) / d(memrealtime) x 100 MHz
+__global__ void __launch_bounds__(256) k_clock(int iters, unsigned long long* out) {
+  __shared__ Fq2 S[2 * 6];
+  const int t = threadIdx.x;
+  if (t < 6) {
+    S[t] = Fq2::one();
+    S[t].c1 = Fq::one();
+  }
+  __syncthreads();
+  Fq2* a = S;
+  Fq2* c = S + 6;
+  const wg::WLane L = wg::wlane_init();
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < iters; i++) {
+    wg::w_sqr(L, c, a);
+    Fq2* tmp = a;
+    a = c;
+    c = tmp;
+  }
+  const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (t == 0) {
+    out[3 * blockIdx.x] = c1 - c0;
+    out[3 * blockIdx.x + 1] = r1 - r0;
+    out[3 * blockIdx.x + 2] = a[0].c0.v[0];
+  }
+}
+
 int main() {
   unsigned long long* dc;
   uint32_t* ds;
@@ -129,7 +168,7 @@ int main() {
     (void)hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
     printf("%-7s %8.1f cycles/op (clock64)\n", names[op], (double)c / iters);
   }
-  for (int mode : {0, 1, 2, 4, 8, 16, 1 | 2 | 4, 1 | 2 | 4 | 8, 31}) {
+  for (int mode : {0, 1, 2, 4, 8, 16, 2 | 4, 1 | 2 | 4, 1 | 2 | 4 | 8, 31}) {
     hipLaunchKernelGGL(k_bench_dbg, dim3(1), dim3(256), 0, 0, mode, 4, dc, ds);
     hipLaunchKernelGGL(k_bench_dbg, dim3(1), dim3(256), 0, 0, mode, iters, dc, ds);
     unsigned long long c = 0;
@@ -140,5 +179,22 @@ int main() {
   unsigned long long c = 0;
   (void)hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
   printf("%-7s %8.1f cycles/op (one wave, dependent Fq products)\n", "fq_mul", (double)c / iters);
+  hipLaunchKernelGGL(k_inv, dim3(1), dim3(64), 0, 0, 2, dc, ds);
+  hipLaunchKernelGGL(k_inv, dim3(1), dim3(64), 0, 0, 20, dc, ds);
+  (void)hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
+  printf("%-7s %8.1f cycles/op (one lane, dependent Fq2 inversions)\n", "fq2_inv", (double)c / 20);
+  for (int grid : {1, 256}) {
+    unsigned long long* dk;
+    (void)hipMalloc(&dk, 3 * 8 * grid);
+    std::vector<unsigned long long> h(3 * grid);
+    hipLaunchKernelGGL(k_clock, dim3(grid), dim3(256), 0, 0, 2000, dk);
+    hipLaunchKernelGGL(k_clock, dim3(grid), dim3(256), 0, 0, 2000, dk);
+    (void)hipMemcpy(h.data(), dk, 3 * 8 * grid, hipMemcpyDeviceToHost);
+    double cyc = 0, rt = 0;
+    for (int b = 0; b < grid; b++) cyc += h[3 * b], rt += h[3 * b + 1];
+    printf("grid %3d: w_sqr %7.1f cycles/op, shader clock %.0f MHz, %.3f us/op\n", grid, cyc / grid / 2000,
+           cyc / rt * 100.0, rt / grid / 2000 / 100.0);
+    (void)hipFree(dk);
+  }
   return 0;
 }

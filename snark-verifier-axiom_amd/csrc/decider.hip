@@ -509,10 +509,10 @@ __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ l
   }
   // final exponentiation (same chain as curve.hpp final_exponentiation)
   // (phases: debug/profiling knob SVGPU_DECIDER_PHASES, 3 = both halves; results are only valid at 3)
+  // inversion-free: the easy part stays the fraction conj(w) / w (see make_wprog below), so this
+  // chain computes W with result conj(W) / W
   Fq2 e = f;
   if (phases & 2) {
-  Fq2 fi = g_inv<S>(G, f);
-  f = g_mul<S>(G, g_conj(G, f), fi);
   f = g_mul<S>(G, g_frob(G, 2, f), f);
   // hard part: f^(l0 + l1 p + l2 p^2 + p^3) with the x-power chain; the small powers of fx and
   // fx^2 share their ladders (fx^6 -> fx^12 -> fx^18, fx2^6 -> fx2^12 -> fx2^18 -> fx2^30)
@@ -546,7 +546,8 @@ __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ l
   const Fq2 l0v = g_conj(G, t);
   e = g_mul<S>(G, g_mul<S>(G, g_mul<S>(G, l0v, g_frob(G, 1, l1v)), g_frob(G, 2, l2v)), g_frob(G, 3, f));
   }
-  const bool one_k = G.k == 0 ? (e == Fq2::one()) : e.is_zero();
+  const bool one_k = (G.k & 1) ? e.is_zero() : true;  // conj(W) == W
+  if (gt && (phases & 2)) e = g_mul<S>(G, g_conj(G, e), g_inv<S>(G, e));  // the Gt value conj(W) / W
   const uint64_t bal = __ballot(one_k || !active);
   const uint64_t gmask = GL == 64 ? ~0ull : ((1ull << GL) - 1);
   const bool ok = ((bal >> (grp * GL)) & gmask) == gmask;
@@ -569,12 +570,12 @@ __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ l
 //   w_sqr    96 lanes (6 coefficients x <= 4 pair terms x <= 4 partial products),
 //   w_frob   24 lanes (6 coefficients x 4),
 // each lane scales its product by its place in the result (the w^6 = xi wrap multiplies by 9 + u),
-// and a coefficient's lanes add up with cross-lane moves (DPP quad/half-row/row mirrors, one
-// ds_swizzle for the 32-lane level) -- no LDS round trip inside an operation.  Operands and results
-// live in LDS slots of 6 Fq2 (the w-basis of fq12_lanes.hpp); an operation never writes a slot it
-// reads (one barrier per operation).  The operations are out-of-line functions: one copy of each
-// in the code object instead of ~60 inlined ones (instruction-cache footprint).  The Miller loop (merged step multipliers) and the final
-// exponentiation are the chain of k_decide_lanes, written over slots.
+// and a coefficient's lanes add up with cross-lane moves (a reduce-scatter of DPP moves and one
+// ds_swizzle for the 32-lane level, lane_sum) -- no LDS round trip inside an operation.  Operands
+// and results live in LDS slots of 6 Fq2 (the w-basis of fq12_lanes.hpp); an operation never
+// writes a slot it reads (one barrier per operation).  The Miller loop (merged step multipliers)
+// and the inversion-free final exponentiation are one straight-line program over the slots
+// (make_wprog), run by an interpreter loop so each operation's code exists once.
 // =============================================================================================
 #ifndef SV_WG_FN
 #define SV_WG_FN __device__ __forceinline__

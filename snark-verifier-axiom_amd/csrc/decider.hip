@@ -608,7 +608,8 @@ __device__ __forceinline__ void st_fq(Fq* p, const Fq& v) {
   q[1] = make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]);
 }
 // Lazily reduced sums: a lane's contribution and the cross-lane partial sums are plain 9-limb
-// integers (every sum here stays below 300 p < 2^263), reduced mod p ONCE per coefficient -- a
+// integers, reduced mod p ONCE per coefficient (lane products and slot values lie in [0, 2p), so a
+// w_mul coefficient sums at most 6 terms x 40 p and a w_sqr one 4 x 80 p: below 330 p < 2^263) -- a
 // cross-lane level then costs one 9-limb carry chain instead of a modular addition, and the xi
 // factor 9 is a shift and an add.
 struct Lz {
@@ -779,7 +780,7 @@ SV_WG_FN void w_mul(const WLane& L, Fq2* __restrict__ dst, const Fq2* a, const F
     // q: 0 a0 b0 (re +), 1 a1 b1 (re -), 2 a0 b1 (im +), 3 a1 b0 (im +)
     const Fq ax = ld_fq((q & 1) ? &a[L.mi].c1 : &a[L.mi].c0);
     const Fq by = ld_fq((q == 1 || q == 2) ? &b[L.mjj].c1 : &b[L.mjj].c0);
-    Fq v = ax * by;
+    Fq v = fe_mul_lazy(ax, by);  // [0, 2p): the lane sums reduce once per coefficient
     if (!L.mact) v = Fq::zero();
     const Fq nv = fq_neg2p(v);
     Lz re, im;
@@ -803,7 +804,7 @@ SV_WG_FN void w_sqr(const WLane& L, Fq2* __restrict__ dst, const Fq2* a) {
     const bool imag = square ? q == 2 : q >= 2;
     const Fq x = ld_fq(xc1 ? &a[L.si].c1 : &a[L.si].c0);
     const Fq y = ld_fq(yc1 ? &a[L.sj].c1 : &a[L.sj].c0);
-    Fq v = x * y;
+    Fq v = fe_mul_lazy(x, y);
     if (!L.slive || (square && q == 3)) v = Fq::zero();
     const Fq nv = fq_neg2p(v);
     const bool neg = q == 1;
@@ -830,7 +831,7 @@ SV_WG_FN void w_frob(Fq2* __restrict__ dst, const Fq2* a, int n, const Fq* gam) 
     Fq x = ld_fq((q & 1) ? &a[kk].c1 : &a[kk].c0);
     if ((n & 1) && (q & 1)) x = fq_neg2p(x);
     const Fq gc = ld_fq(gam + ((n - 1) * 6 + kk) * 2 + ((q == 1 || q == 2) ? 1 : 0));
-    Fq v = x * gc;
+    Fq v = fe_mul_lazy(x, gc);
     if (!act) v = Fq::zero();
     const Fq nv = fq_neg2p(v);
     Lz re, im;

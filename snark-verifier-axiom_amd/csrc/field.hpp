@@ -269,8 +269,9 @@ __device__ __forceinline__ void mac_first4(uint64_t& acc, uint32_t& ovf, const u
 
 // Montgomery multiplication by finely integrated product scanning: column k accumulates
 // a_i b_{k-i} and m_i p_{k-i} in (acc, ovf); for k < 8 the column's low word fixes m_k.
-template <class M>
-SV_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
+// kReduce = false skips the final conditional subtraction (fe_mul_lazy).
+template <class M, bool kReduce>
+SV_HD Fe<M> mont_mul(const Fe<M>& a, const Fe<M>& b) {
   uint32_t m[8], t[8];
   uint64_t acc = 0;
   uint32_t ovf = 0;
@@ -331,6 +332,13 @@ SV_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
     acc = (acc >> 32) | ((uint64_t)ovf << 32);
   }
   const uint32_t top = (uint32_t)acc;
+  if constexpr (!kReduce) {
+    Fe<M> r;
+#pragma unroll
+    for (int j = 0; j < 8; j++) r.v[j] = t[j];
+    (void)top;
+    return r;
+  }
   Fe<M> d;
   uint64_t br = 0;
 #pragma unroll
@@ -344,6 +352,16 @@ SV_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
 #pragma unroll
   for (int j = 0; j < 8; j++) r.v[j] = ge ? d.v[j] : t[j];
   return r;
+}
+template <class M>
+SV_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
+  return mont_mul<M, true>(a, b);
+}
+// Montgomery product WITHOUT the final conditional subtraction: for a, b < 2p the result is below
+// 2p (4 p^2 < 2^256 p), which is all a lazily reduced consumer needs (the decider's lane sums).
+template <class M>
+SV_HD Fe<M> fe_mul_lazy(const Fe<M>& a, const Fe<M>& b) {
+  return mont_mul<M, false>(a, b);
 }
 #else
 // CIOS Montgomery multiplication (host build of the same templates): r = a * b * 2^-256 mod m.
@@ -390,6 +408,10 @@ SV_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
 #pragma unroll
   for (int j = 0; j < 8; j++) r.v[j] = ge ? d.v[j] : t[j];
   return r;
+}
+template <class M>
+SV_HD Fe<M> fe_mul_lazy(const Fe<M>& a, const Fe<M>& b) {
+  return a * b;
 }
 #endif
 

@@ -710,7 +710,9 @@ __device__ __forceinline__ Lz lane_sum(const Lz& re, const Lz& im) {
   if constexpr (LEVELS > 1) v = lz_add(v, xmove<1>(v));
   if constexpr (LEVELS > 2) v = lz_add(v, xmove<5>(v));
   if constexpr (LEVELS > 3) v = lz_add(v, xmove<6>(v));
-  // (lane ^ 16 by v_permlane16_swap instead of ds_swizzle measured the same: 3611 vs 3554 cycles)
+  // (lane ^ 16 by v_permlane16_swap instead of ds_swizzle measured the same: 3611 vs 3554 cycles;
+  // folding the moves into v_addc_co_u32_dpp chains was slower, 0.670 -> 0.679 ms: back-to-back
+  // v_addc need s_nop 1 between them, which the interleaved v_mov_dpp otherwise fill)
   if constexpr (LEVELS > 4) v = lz_add(v, xmove<4>(v));
   return v;
 }

@@ -89,6 +89,34 @@ SV_HD G1Xyzz xyzz_madd_aff(const G1Xyzz& p, const G1Aff& q) {
   return xyzz_madd(p, q.x, q.y);
 }
 
+// madd-2008-s with the accumulator kept in the 2p domain (coordinates in [0, 2p), field.hpp): the
+// products skip their final conditional subtraction, 2Q is subtracted as Q twice, and the
+// degenerate-case tests compare against both representatives of 0.  Y3 = Rd (Q - X3) - Y PPP is
+// one fused sum of two products of inputs below 2p: below 2.52 p before, 1.52 p after its
+// subtraction.  For the bucket accumulation chain (k_accumulate), which canonicalises before every
+// store (xyzz_canon2p); (x2, y2) is a reduced affine point, not the identity.
+SV_HD G1Xyzz xyzz_madd_2p(const G1Xyzz& p, const Fq& x2, const Fq& y2) {
+  if (p.is_identity()) return {x2, y2, Fq::one(), Fq::one()};
+  const Fq U2 = fe_mul_lazy(x2, p.ZZ);
+  const Fq S2 = fe_mul_lazy(y2, p.ZZZ);
+  const Fq Pd = fe_sub2p(U2, p.X);
+  const Fq Rd = fe_sub2p(S2, p.Y);
+  if (fe_is_zero2p(Pd)) {
+    if (fe_is_zero2p(Rd)) return xyzz_mdbl(x2, y2);
+    return G1Xyzz::identity();
+  }
+  const Fq PP = fe_sqr_hp<FqTag, false>(Pd);
+  const Fq PPP = fe_mul_lazy(Pd, PP);
+  const Fq Q = fe_mul_lazy(p.X, PP);
+  const Fq X3 = fe_sub2p(fe_sub2p(fe_sub2p(fe_sqr_hp<FqTag, false>(Rd), PPP), Q), Q);
+  const Fq x[2] = {Rd, p.Y};
+  const Fq y[2] = {fe_sub2p(Q, X3), fe_neg2p(PPP)};
+  return {X3, fe_mul_sum(x, y), fe_mul_lazy(p.ZZ, PP), fe_mul_lazy(p.ZZZ, PPP)};
+}
+SV_HD G1Xyzz xyzz_canon2p(const G1Xyzz& p) {
+  return {fe_canon2p(p.X), fe_canon2p(p.Y), fe_canon2p(p.ZZ), fe_canon2p(p.ZZZ)};
+}
+
 // add-2008-s
 SV_HD G1Xyzz xyzz_add(const G1Xyzz& p, const G1Xyzz& q) {
   if (p.is_identity()) return q;

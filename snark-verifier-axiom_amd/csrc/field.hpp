@@ -424,7 +424,7 @@ SV_HD Fe<M> fe_mul_lazy(const Fe<M>& a, const Fe<M>& b) {
 // adding a doubled word cannot overflow the 64-bit accumulator.  Measured: k_accumulate 1.52 ->
 // 1.49 ms at 2^20; single-wave chains (decider, batched Horner) were ~1 % slower with it (two
 // dependent scans), so fe_sqr stays a * a and only the XYZZ formulas and Poseidon use fe_sqr_hp.
-template <class M>
+template <class M, bool kReduce = true>
 SV_HD Fe<M> fe_sqr_hp(const Fe<M>& a) {
   uint32_t od[16];
   uint64_t acc = 0;
@@ -522,6 +522,13 @@ SV_HD Fe<M> fe_sqr_hp(const Fe<M>& a) {
     acc = (acc >> 32) | ((uint64_t)ovf << 32);
   }
   const uint32_t top = (uint32_t)acc;
+  if constexpr (!kReduce) {  // [0, 2p) for inputs below 2p (fe_mul_lazy)
+    Fe<M> r;
+#pragma unroll
+    for (int j = 0; j < 8; j++) r.v[j] = t[j];
+    (void)top;
+    return r;
+  }
   Fe<M> dd;
   uint64_t br = 0;
 #pragma unroll
@@ -537,11 +544,78 @@ SV_HD Fe<M> fe_sqr_hp(const Fe<M>& a) {
   return r;
 }
 #else
-template <class M>
+template <class M, bool kReduce = true>
 SV_HD Fe<M> fe_sqr_hp(const Fe<M>& a) {
   return a * a;
 }
 #endif
+
+// ---- the 2p domain: values in [0, 2p), as lazily reduced chains keep them (k_accumulate's
+// bucket additions, the decider's lane products).  2p < 2^255 for both BN254 moduli.
+template <class M>
+SV_HD uint32_t p2_limb(int i) {
+  return (M::p(i) << 1) | (i ? M::p(i - 1) >> 31 : 0u);
+}
+// carry chains through the clang builtins (v_addc / v_subb on the device); 64-bit C for g++
+SV_HD uint32_t sv_addc(uint32_t a, uint32_t b, uint32_t c, uint32_t* co) {
+#if defined(__clang__)
+  return __builtin_addc(a, b, c, co);
+#else
+  const uint64_t s = (uint64_t)a + b + c;
+  *co = (uint32_t)(s >> 32);
+  return (uint32_t)s;
+#endif
+}
+SV_HD uint32_t sv_subc(uint32_t a, uint32_t b, uint32_t c, uint32_t* co) {
+#if defined(__clang__)
+  return __builtin_subc(a, b, c, co);
+#else
+  const uint64_t s = (uint64_t)a - b - c;
+  *co = (uint32_t)(s >> 63);
+  return (uint32_t)s;
+#endif
+}
+// a - b for a, b in [0, 2p): + 2p on borrow
+template <class M>
+SV_HD Fe<M> fe_sub2p(const Fe<M>& a, const Fe<M>& b) {
+  Fe<M> t, r;
+  uint32_t c = 0, br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) t.v[i] = sv_subc(a.v[i], b.v[i], br, &br);
+  const uint32_t mask = 0u - br;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = sv_addc(t.v[i], p2_limb<M>(i) & mask, c, &c);
+  return r;
+}
+// 2p - a for a in [0, 2p]
+template <class M>
+SV_HD Fe<M> fe_neg2p(const Fe<M>& a) {
+  Fe<M> r;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = sv_subc(p2_limb<M>(i), a.v[i], br, &br);
+  return r;
+}
+// [0, 2p) -> [0, p)
+template <class M>
+SV_HD Fe<M> fe_canon2p(const Fe<M>& a) {
+  Fe<M> d;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) d.v[i] = sv_subc(a.v[i], M::p(i), br, &br);
+  return br ? a : d;
+}
+// a == 0 (mod p) for a in [0, 2p)
+template <class M>
+SV_HD bool fe_is_zero2p(const Fe<M>& a) {
+  uint32_t z = 0, e = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    z |= a.v[i];
+    e |= a.v[i] ^ M::p(i);
+  }
+  return z == 0 || e == 0;
+}
 
 template <class M>
 SV_HD Fe<M> fe_sqr(const Fe<M>& a) {

@@ -557,6 +557,7 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
 #endif
     for (uint32_t e = s0; e < e_end; e++) {
       if (e >= ge) {  // segment [seg_start, ge) of bucket g ends inside this chunk
+        acc = xyzz_canon2p(acc);
         if (seg_start == gs) {
           store_xyzz(bsum, g, acc);
         } else {  // head piece of a bucket owned by an earlier thread
@@ -590,8 +591,9 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
       }
 #endif
       if (v & 0x80000000u) p.y = -p.y;
-      acc = xyzz_madd_aff(acc, p);
+      if (!p.is_identity()) acc = xyzz_madd_2p(acc, p.x, p.y);
     }
+    acc = xyzz_canon2p(acc);
     if (seg_start == gs && e_end == ge) {
       store_xyzz(bsum, g, acc);
     } else if (seg_start != gs) {  // first segment, bucket started earlier (it may also go on later)
@@ -863,25 +865,27 @@ MsmPlan msm_plan(size_t n) {
     SV_LAUNCH_C1(KERNEL, 255, C, GRID, BLOCK, __VA_ARGS__)         \
   }
 
-// Host Horner over (window, group) terms: total = sum_w 2^(c w) [A_lo + A_hi + sum_k 2^(2+k) U_k].
-static host::Xyzz host_combine_part(const MsmPlan& p, const host::Xyzz* A /* [W][NG] */, uint32_t w0, uint32_t w1,
-                                    host::Xyzz acc) {
-  const int top = w1 == p.W ? (int)(p.c * (p.W - 1) + p.logL + p.logJ) : (int)(p.c * w1 - 1);
-  const int bot = (int)(p.c * w0);
-  std::vector<host::Xyzz> byexp(top - bot + 1, host::x_identity());
-  for (uint32_t w = w0; w < w1; w++)
-    for (uint32_t q = 0; q < p.NG; q++) {
-      int e = (int)(p.c * w + (q < 2 ? 0 : p.logL + (q - 2)));
-      byexp[e - bot] = host::x_add(byexp[e - bot], A[w * p.NG + q]);
-    }
-  for (int e = top; e >= bot; e--) {
-    acc = host::x_dbl(acc);
-    acc = host::x_add(acc, byexp[e - bot]);
+// Host Horner over (window, group) terms: total = sum_w 2^(c w) [A_lo + A_hi + 2^logL sum_k 2^k U_k]
+// (k < logJ; J >= 4, so every window has U terms): each window's S_w by its own Horner (27 point
+// operations), then the Horner over windows (c (W - 1) doublings) -- 690 point operations instead
+// of 740 for one Horner over every exponent.  (Running the windows' S_w on the host pool cost more
+// than it saved: waking the pool per MSM, and its spinning workers then slowed the caller's next
+// launches -- 2.27 -> 2.52 ms per step at 2^20.)
+static host::Xyzz host_combine(const MsmPlan& p, const host::Xyzz* A) {
+  std::vector<host::Xyzz> S(p.W);
+  for (uint32_t w = 0; w < p.W; w++) {
+    const host::Xyzz* a = A + w * p.NG;
+    host::Xyzz acc = a[p.NG - 1];
+    for (int q = (int)p.NG - 2; q >= 2; q--) acc = host::x_add(host::x_dbl(acc), a[q]);
+    for (uint32_t i = 0; i < p.logL; i++) acc = host::x_dbl(acc);
+    S[w] = host::x_add(host::x_add(acc, a[0]), a[1]);
+  }
+  host::Xyzz acc = S[p.W - 1];
+  for (int w = (int)p.W - 2; w >= 0; w--) {
+    for (int i = 0; i < p.c; i++) acc = host::x_dbl(acc);
+    acc = host::x_add(acc, S[w]);
   }
   return acc;
-}
-static host::Xyzz host_combine(const MsmPlan& p, const host::Xyzz* A) {
-  return host_combine_part(p, A, 0, p.W, host::x_identity());
 }
 
 // One piece's front half: digits + two-level sort + bucket accumulation + crossing-bucket fixups

@@ -116,6 +116,30 @@ SV_HD G1Xyzz xyzz_madd_2p(const G1Xyzz& p, const Fq& x2, const Fq& y2) {
 SV_HD G1Xyzz xyzz_canon2p(const G1Xyzz& p) {
   return {fe_canon2p(p.X), fe_canon2p(p.Y), fe_canon2p(p.ZZ), fe_canon2p(p.ZZZ)};
 }
+// add-2008-s in the 2p domain (both inputs in [0, 2p); the identity is exactly ZZ = 0): the bucket
+// reduction chains (k_wsum, k_group_sum), canonical at their stores.
+SV_HD G1Xyzz xyzz_add_2p(const G1Xyzz& p, const G1Xyzz& q) {
+  if (p.is_identity()) return q;
+  if (q.is_identity()) return p;
+  const Fq U1 = fe_mul_lazy(p.X, q.ZZ);
+  const Fq U2 = fe_mul_lazy(q.X, p.ZZ);
+  const Fq S1 = fe_mul_lazy(p.Y, q.ZZZ);
+  const Fq S2 = fe_mul_lazy(q.Y, p.ZZZ);
+  const Fq Pd = fe_sub2p(U2, U1);
+  const Fq Rd = fe_sub2p(S2, S1);
+  if (fe_is_zero2p(Pd)) {
+    if (fe_is_zero2p(Rd)) return xyzz_dbl(xyzz_canon2p(p));
+    return G1Xyzz::identity();
+  }
+  const Fq PP = fe_sqr_hp<FqTag, false>(Pd);
+  const Fq PPP = fe_mul_lazy(Pd, PP);
+  const Fq Q = fe_mul_lazy(U1, PP);
+  const Fq X3 = fe_sub2p(fe_sub2p(fe_sub2p(fe_sqr_hp<FqTag, false>(Rd), PPP), Q), Q);
+  const Fq x[2] = {Rd, S1};
+  const Fq y[2] = {fe_sub2p(Q, X3), fe_neg2p(PPP)};
+  return {X3, fe_mul_sum(x, y), fe_mul_lazy(fe_mul_lazy(p.ZZ, q.ZZ), PP),
+          fe_mul_lazy(fe_mul_lazy(p.ZZZ, q.ZZZ), PPP)};
+}
 
 // add-2008-s
 SV_HD G1Xyzz xyzz_add(const G1Xyzz& p, const G1Xyzz& q) {

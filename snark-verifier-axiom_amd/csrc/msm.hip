@@ -722,13 +722,13 @@ __global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, c
         i = ci - 1;
         ne = bucket_at(x, gs, i, nx);
       }
-      if (cne) run = xyzz_add(run, cur);
-      if (base || ci > lo) acc = xyzz_add(acc, run);
+      if (cne) run = xyzz_add_2p(run, cur);
+      if (base || ci > lo) acc = xyzz_add_2p(acc, run);
       if (ci == lo) break;
     }
   }
-  store_xyzz(acc_out, tid, acc);
-  if (tot_out) store_xyzz(tot_out, tid, run);
+  store_xyzz(acc_out, tid, xyzz_canon2p(acc));
+  if (tot_out) store_xyzz(tot_out, tid, xyzz_canon2p(run));
 }
 
 // Step 2 fused: one 512-thread block per (window, group) sums the group's H members (strided,
@@ -750,15 +750,15 @@ __global__ void __launch_bounds__(kGroupBlock) k_group_sum(const G1Xyzz* __restr
       const uint32_t j = ((m >> k) << (k + 1)) | (1u << k) | (m & ((1u << k) - 1));
       x = load_xyzz(tot, w * J + j);
     }
-    s = xyzz_add(s, x);
+    s = xyzz_add_2p(s, x);
   }
   sh[tid] = s;
   __syncthreads();
   for (uint32_t st = kGroupBlock / 2; st > 0; st >>= 1) {
-    if (tid < st) sh[tid] = xyzz_add(sh[tid], sh[tid + st]);
+    if (tid < st) sh[tid] = xyzz_add_2p(sh[tid], sh[tid + st]);
     __syncthreads();
   }
-  if (tid == 0) store_xyzz(out, gid, sh[0]);
+  if (tid == 0) store_xyzz(out, gid, xyzz_canon2p(sh[0]));
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -63,9 +63,11 @@ __device__ __forceinline__ Fr ld_const(const uint32_t* p) {
   return r;
 }
 
+// x^5 with the two squares left in [0, 2p) (field.hpp's 2p domain): only the result, which
+// feeds the fused MDS sums, is fully reduced
 __device__ __forceinline__ Fr pow5(const Fr& x) {
-  const Fr x2 = fe_sqr_hp(x);
-  return fe_sqr_hp(x2) * x;
+  const Fr x2 = fe_sqr_hp<FrTag, false>(x);
+  return fe_sqr_hp<FrTag, false>(x2) * x;
 }
 
 // One MDS row, sum_j s_j M_ij, as fused sums of up to three products with one Montgomery reduction

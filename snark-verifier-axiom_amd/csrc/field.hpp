@@ -587,6 +587,20 @@ SV_HD Fe<M> fe_sub2p(const Fe<M>& a, const Fe<M>& b) {
   for (int i = 0; i < 8; i++) r.v[i] = sv_addc(t.v[i], p2_limb<M>(i) & mask, c, &c);
   return r;
 }
+// a + b for a, b in [0, 2p): - 2p when the sum reaches 2p (4p < 2^256: no carry out)
+template <class M>
+SV_HD Fe<M> fe_add2p(const Fe<M>& a, const Fe<M>& b) {
+  Fe<M> t, d, r;
+  uint32_t c = 0, br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    t.v[i] = sv_addc(a.v[i], b.v[i], c, &c);
+    d.v[i] = sv_subc(t.v[i], p2_limb<M>(i), br, &br);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = br ? t.v[i] : d.v[i];
+  return r;
+}
 // 2p - a for a in [0, 2p]
 template <class M>
 SV_HD Fe<M> fe_neg2p(const Fe<M>& a) {

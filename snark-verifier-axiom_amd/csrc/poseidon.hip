@@ -63,11 +63,15 @@ __device__ __forceinline__ Fr ld_const(const uint32_t* p) {
   return r;
 }
 
-// x^5 with the two squares left in [0, 2p) (field.hpp's 2p domain): only the result, which
-// feeds the fused MDS sums, is fully reduced
+// The permutation runs in field.hpp's 2p domain: every state word stays in [0, 2r) (r < 2^254 is
+// the Fr modulus), so no product pays its final conditional subtraction.  Bounds (R = 2^256,
+// r < 0.19 R): a product of words below 2r is below (4 r^2 + R r) / R < 1.76 r; an MDS row, a fused
+// sum of three products of words below 2r with constants below r, scans below
+// (6 r^2 + R r) / R < 2.14 r and leaves fe_mul_sum's single subtraction below 1.14 r; adding a
+// constant (< r) wraps at 2r (fe_add2p).  The result is canonicalised at the end.
 __device__ __forceinline__ Fr pow5(const Fr& x) {
   const Fr x2 = fe_sqr_hp<FrTag, false>(x);
-  return fe_sqr_hp<FrTag, false>(x2) * x;
+  return fe_mul_lazy(fe_sqr_hp<FrTag, false>(x2), x);
 }
 
 // One MDS row, sum_j s_j M_ij, as fused sums of up to three products with one Montgomery reduction
@@ -104,7 +108,7 @@ __device__ __forceinline__ void apply_mds(Fr (&s)[T], const uint32_t* m) {
 template <int T>
 __device__ __forceinline__ void full_round(Fr (&s)[T], const uint32_t* c, const uint32_t* m) {
 #pragma unroll
-  for (int i = 0; i < T; i++) s[i] = c ? pow5(s[i]) + ld_const(c + i * 8) : pow5(s[i]);
+  for (int i = 0; i < T; i++) s[i] = c ? fe_add2p(pow5(s[i]), ld_const(c + i * 8)) : pow5(s[i]);
   apply_mds<T>(s, m);
 }
 
@@ -121,16 +125,18 @@ __device__ __forceinline__ void permute(Fr (&s)[T]) {
   const uint32_t* partial = PSpec<T>::partial();
   const uint32_t* sparse = PSpec<T>::sparse();
   for (int r = 0; r < RP; r++) {
-    s[0] = pow5(s[0]) + ld_const(partial + r * 8);
+    s[0] = fe_add2p(pow5(s[0]), ld_const(partial + r * 8));
     const uint32_t* row = sparse + r * (2 * T - 1) * 8;
     const Fr s0 = mds_row<T>(s, row);
 #pragma unroll
-    for (int i = 1; i < T; i++) s[i] = s[i] + s[0] * ld_const(row + (T + i - 1) * 8);
+    for (int i = 1; i < T; i++) s[i] = fe_add2p(s[i], fe_mul_lazy(s[0], ld_const(row + (T + i - 1) * 8)));
     s[0] = s0;
   }
   const uint32_t* end = PSpec<T>::end();
   for (int r = 0; r < H - 1; r++) full_round<T>(s, end + r * T * 8, PSpec<T>::mds());
   full_round<T>(s, nullptr, PSpec<T>::mds());
+#pragma unroll
+  for (int i = 0; i < T; i++) s[i] = fe_canon2p(s[i]);
 }
 
 __device__ __forceinline__ Fr load_fr(const Fr* p, int mont) {

@@ -208,9 +208,9 @@ __global__ void __launch_bounds__(kThreads) k_msm_batch_windows(const G1Aff* __r
             }
             if ((e >> 8) & 1) x = x * beta;  // phi(P) = (beta x, y)
             if (e >> 15) y = -y;
-            acc = xyzz_madd(acc, x, y);
+            acc = xyzz_madd_2p(acc, x, y);  // 2p domain (curve.hpp), canonical before smul_small
           }
-          if (!acc.is_identity()) part = xyzz_add(part, smul_small(acc, (uint32_t)b + 1));
+          if (!acc.is_identity()) part = xyzz_add(part, smul_small(xyzz_canon2p(acc), (uint32_t)b + 1));
         }
       }
 #pragma unroll
@@ -476,14 +476,14 @@ __global__ void __launch_bounds__(kThreads) k_msm_batch_fixed(const G1Aff* __res
       a.y = ld_fq(qp + 8);
       if (a.x.is_zero() && a.y.is_zero()) continue;  // identity row
       if (e & 1) a.y = -a.y;
-      acc = xyzz_madd_aff(acc, a);
+      acc = xyzz_madd_2p(acc, a.x, a.y);  // the bucket sums stay in the 2p domain (curve.hpp)
     }
     __syncthreads();
   }
   // S_b = the two halves of bucket b
   if (part == 1) T[bucket] = acc;
   __syncthreads();
-  if (part == 0) T[bucket] = xyzz_add(acc, T[bucket]);
+  if (part == 0) T[bucket] = xyzz_add_2p(acc, T[bucket]);
   __syncthreads();
   // suffix sums T_k = sum_{b >= k} S_b (Hillis-Steele, 7 levels)
   for (int d = 1; d < kFixB; d <<= 1) {
@@ -491,16 +491,16 @@ __global__ void __launch_bounds__(kThreads) k_msm_batch_fixed(const G1Aff* __res
     const bool live = tid < kFixB && tid + d < kFixB;
     if (live) v = T[tid + d];
     __syncthreads();
-    if (live) T[tid] = xyzz_add(T[tid], v);
+    if (live) T[tid] = xyzz_add_2p(T[tid], v);
     __syncthreads();
   }
   // sum_b (b + 1) S_b = sum_k T_k (tree, 7 levels)
   for (int h = kFixB / 2; h >= 1; h >>= 1) {
-    if (tid < h) T[tid] = xyzz_add(T[tid], T[tid + h]);
+    if (tid < h) T[tid] = xyzz_add_2p(T[tid], T[tid + h]);
     __syncthreads();
   }
   if (tid == 0) {
-    const G1Xyzz r = T[0];
+    const G1Xyzz r = xyzz_canon2p(T[0]);
     G1Aff a = xyzz_to_affine(r);
     if (!mont && !r.is_identity()) {
       a.x = fe_from_mont(a.x);

@@ -641,7 +641,9 @@ SV_HD Fe<M> fe_sqr(const Fe<M>& a) {
 // a_n,i b_n,k-i for every pair n and then m_i p_k-i, so N products cost 64 N + 64 multiply-adds
 // instead of 128 N.  With p < 2^254 the scanned value is below (N p^2 + 2^256 p) / 2^256 < 2p for
 // N <= 3, so the single conditional subtraction of operator* still reduces fully.
-template <class M, int N>
+// kReduce = false returns the scanned value itself (below 2^256 for the operand bounds the caller
+// states; no final subtraction), as fe_mul_lazy does for one product.
+template <class M, int N, bool kReduce = true>
 SV_HD Fe<M> fe_mul_sum(const Fe<M> (&a)[N], const Fe<M> (&b)[N]) {
   static_assert(N >= 1 && N <= 3, "fe_mul_sum: the final subtraction covers N <= 3");
   uint32_t m[8], t[8];
@@ -702,6 +704,12 @@ SV_HD Fe<M> fe_mul_sum(const Fe<M> (&a)[N], const Fe<M> (&b)[N]) {
     }
     acc = (acc >> 32) | ((uint64_t)ovf << 32);
   }
+  if constexpr (!kReduce) {
+    Fe<M> r;
+#pragma unroll
+    for (int j = 0; j < 8; j++) r.v[j] = t[j];
+    return r;
+  }
   const uint32_t top = (uint32_t)acc;
   Fe<M> d;
   uint64_t br = 0;
@@ -718,7 +726,7 @@ SV_HD Fe<M> fe_mul_sum(const Fe<M> (&a)[N], const Fe<M> (&b)[N]) {
   return r;
 }
 #else
-template <class M, int N>
+template <class M, int N, bool kReduce = true>
 SV_HD Fe<M> fe_mul_sum(const Fe<M> (&a)[N], const Fe<M> (&b)[N]) {
   Fe<M> r = a[0] * b[0];
   for (int n = 1; n < N; n++) r = r + a[n] * b[n];

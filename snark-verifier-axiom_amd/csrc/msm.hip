@@ -59,6 +59,23 @@ __device__ __forceinline__ G1Aff load_aff(const G1Aff* __restrict__ a, uint32_t 
   return r;
 }
 
+// virtual point idx: P_idx, or phi(P_(idx - nsplit)) = (beta x, y) for a GLV k2 entry (nsplit = n;
+// ~0u without GLV): x from the beta-x table, y from the bases
+__device__ __forceinline__ G1Aff load_vpoint(const G1Aff* __restrict__ bases, const uint4* __restrict__ phix,
+                                             uint32_t idx, uint32_t nsplit) {
+  const bool ph = idx >= nsplit;
+  const uint32_t i = ph ? idx - nsplit : idx;
+  const uint4* p = reinterpret_cast<const uint4*>(bases + i);
+  const uint4* px = ph ? phix + 2 * i : p;
+  const uint4 q0 = px[0], q1 = px[1], q2 = p[2], q3 = p[3];
+  G1Aff r;
+  r.x.v[0] = q0.x; r.x.v[1] = q0.y; r.x.v[2] = q0.z; r.x.v[3] = q0.w;
+  r.x.v[4] = q1.x; r.x.v[5] = q1.y; r.x.v[6] = q1.z; r.x.v[7] = q1.w;
+  r.y.v[0] = q2.x; r.y.v[1] = q2.y; r.y.v[2] = q2.z; r.y.v[3] = q2.w;
+  r.y.v[4] = q3.x; r.y.v[5] = q3.y; r.y.v[6] = q3.z; r.y.v[7] = q3.w;
+  return r;
+}
+
 __device__ __forceinline__ G1Xyzz load_xyzz(const G1Xyzz* __restrict__ a, uint32_t i) {
   const uint4* p = reinterpret_cast<const uint4*>(a + i);
   G1Xyzz r;
@@ -139,37 +156,58 @@ __device__ __forceinline__ Fr load_scalar(const Fr* __restrict__ scalars, uint32
   return mont_in ? fe_from_mont(s) : s;
 }
 
-// Scalar of virtual point i for the sort passes: a full scalar (NB = 255), or a GLV half (NB = 128,
-// glv_pack layout: 127-bit magnitude, sign in bit 31 of limb 3 -> sgn, folded into every digit).
-template <int NB>
-__device__ __forceinline__ Fr load_digits_src(const void* __restrict__ src, uint32_t i, int mont_in,
-                                              uint32_t* __restrict__ err, uint32_t& sgn) {
-  if constexpr (NB == 255) {
-    sgn = 0;
-    return load_scalar(reinterpret_cast<const Fr*>(src), i, mont_in, err);
-  } else {
-    const uint4 q = reinterpret_cast<const uint4*>(src)[i];
-    Fr s;
-    s.v[0] = q.x; s.v[1] = q.y; s.v[2] = q.z; s.v[3] = q.w & 0x7fffffffu;
-    s.v[4] = 0; s.v[5] = 0; s.v[6] = 0; s.v[7] = 0;
-    sgn = q.w >> 31;
-    return s;
+// Entries of real point i for the sort passes.  Without GLV: the W signed digits of its scalar,
+// all for virtual point i (half 0).  With GLV the scalar is split here (glv.hpp; nothing is
+// stored): the W digits of k1 belong to virtual point i (P_i, half 0) and the W digits of k2 to
+// virtual point n + i (phi(P_i), half 1), each half's sign folded into its digits' signs; both
+// halves share the W windows' buckets.  f(w, mag, neg, half) per digit.
+template <int C, bool GLV>
+struct Digits {
+  static constexpr int NB = GLV ? 128 : 255;
+  static constexpr int W = num_windows<C, NB>();
+  static constexpr int EP = GLV ? 2 * W : W;  // entries per real point
+  uint32_t h[GLV ? 2 : 1][GLV ? 4 : 8];
+  uint32_t sgn[GLV ? 2 : 1];
+  __device__ __forceinline__ void load(const Fr* __restrict__ scalars, uint32_t i, int mont_in,
+                                       uint32_t* __restrict__ err) {
+    const Fr s = load_scalar(scalars, i, mont_in, err);
+    if constexpr (GLV) {
+      uint32_t h1[4], h2[4];
+      glv_split(s.v, h1, h2);
+#pragma unroll
+      for (int k = 0; k < 4; k++) h[0][k] = h1[k], h[1][k] = h2[k];
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        sgn[q] = h[q][3] >> 31;
+        h[q][3] &= 0x7fffffffu;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; k++) h[0][k] = s.v[k];
+      sgn[0] = 0;
+    }
   }
-}
+  template <class F>
+  __device__ __forceinline__ void each(F&& f) const {
+#pragma unroll
+    for (int q = 0; q < (GLV ? 2 : 1); q++) {
+      Fr s;
+      if constexpr (GLV) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) s.v[k] = h[q][k], s.v[4 + k] = 0u;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++) s.v[k] = h[0][k];
+      }
+      const uint32_t sg = sgn[q];
+      for_each_digit<C, NB>(s, [&](int w, uint32_t mag, uint32_t neg) { f(w, mag, neg ^ sg, (uint32_t)q); });
+    }
+  }
+};
 
-// GLV preparation (glv.hpp): scalar k_i -> halves (k1, k2) stored as hs[i], hs[n + i]; the
-// endomorphism image phi(P_i) = (beta x_i, y_i) stored as phi[i] (identity (0, 0) maps to itself).
-// The sort and accumulate passes then run over 2n virtual points with 128-bit scalars.
-__global__ void k_glv_prep(const G1Aff* __restrict__ bases, const Fr* __restrict__ scalars, uint32_t n,
-                           int mont_in, uint4* __restrict__ hs, G1Aff* __restrict__ phi,
-                           uint32_t* __restrict__ err) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const Fr k = load_scalar(scalars, i, mont_in, err);
-  uint32_t h1[4], h2[4];
-  glv_split(k.v, h1, h2);
-  hs[i] = make_uint4(h1[0], h1[1], h1[2], h1[3]);
-  hs[n + i] = make_uint4(h2[0], h2[1], h2[2], h2[3]);
+// GLV: phi(P_i) = (beta x_i, y_i); only beta x_i is stored (phix[i], 32 B, written by k_bin_hist),
+// the accumulate reads y_i from the bases (identity (0, 0) maps to itself).
+__device__ __forceinline__ void glv_phix(const G1Aff* __restrict__ bases, uint32_t i, uint4* __restrict__ phix) {
   const uint4* b = reinterpret_cast<const uint4*>(bases + i);
   Fq x, beta;
   const uint4 x0 = b[0], x1 = b[1];
@@ -178,11 +216,8 @@ __global__ void k_glv_prep(const G1Aff* __restrict__ bases, const Fr* __restrict
 #pragma unroll
   for (int j = 0; j < 8; j++) beta.v[j] = GLV_BETA_MONT[j];
   const Fq bx = x * beta;
-  uint4* o = reinterpret_cast<uint4*>(phi + i);
-  o[0] = make_uint4(bx.v[0], bx.v[1], bx.v[2], bx.v[3]);
-  o[1] = make_uint4(bx.v[4], bx.v[5], bx.v[6], bx.v[7]);
-  o[2] = b[2];
-  o[3] = b[3];
+  phix[2 * i] = make_uint4(bx.v[0], bx.v[1], bx.v[2], bx.v[3]);
+  phix[2 * i + 1] = make_uint4(bx.v[4], bx.v[5], bx.v[6], bx.v[7]);
 }
 
 // ---- two-level counting sort of the n * W (point, digit) entries by bucket ------------------
@@ -197,7 +232,7 @@ __global__ void k_glv_prep(const G1Aff* __restrict__ bases, const Fr* __restrict
 // accumulate chunk [tK, tK + K).  No per-(window, point) digit array is ever stored.
 // points per block in passes 1 and 3: 512 (2 per thread), 256 when the LDS staging of W digits
 // per point would not fit (small c, many windows)
-__host__ __device__ constexpr uint32_t sort_chunk(int c, int nb = 255) { return (nb + c - 1) / c > 20 ? 256u : 512u; }
+__host__ __device__ constexpr uint32_t sort_chunk(int ep) { return ep > 20 ? 256u : 512u; }  // ep: entries per point
 // coarse bits: 2^CB bins per window, so that W * 2^CB ~ 1024 fine-sort regions of ~16K entries at
 // 2^20 (LDS-staged in k_fine_sort) -- 64 bins for the 16 full-width windows, 128 for the 8 GLV ones
 __host__ __device__ constexpr int coarse_bits(int c, int nb) { return c - 1 < (nb == 128 ? 7 : 6) ? c - 1 : (nb == 128 ? 7 : 6); }
@@ -236,21 +271,39 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t* x, uint32_t* part)
   return total;
 }
 
-template <int C, int NB>
-__global__ void __launch_bounds__(kBlock) k_bin_hist(const void* __restrict__ scalars, uint32_t n, int mont_in,
+// Coarse-binned entries (tmp[]): u64 fine << 32 | point | sign << 31, or -- when the virtual
+// point index fits in 31 - FB bits (every size up to 2^22 points) -- packed into u32 as
+// fine << (32 - FB) | sign << (31 - FB) | point, which halves the scatter's writes and the fine
+// sort's reads.  The fine sort expands either form to the u64 layout in registers.
+__device__ __forceinline__ uint32_t pack_entry32(uint32_t fine, uint32_t neg, uint32_t pt, uint32_t fb) {
+  return (fb ? fine << (32 - fb) : 0u) | (neg << (31 - fb)) | pt;
+}
+__device__ __forceinline__ uint64_t load_entry(const uint64_t* __restrict__ tmp, uint32_t i, int e32, uint32_t fb) {
+  if (!e32) return tmp[i];
+  const uint32_t v = reinterpret_cast<const uint32_t*>(tmp)[i];
+  const uint32_t fine = fb ? v >> (32 - fb) : 0u, neg = (v >> (31 - fb)) & 1u, pt = v & ((1u << (31 - fb)) - 1u);
+  return ((uint64_t)fine << 32) | pt | (neg << 31);
+}
+
+// With GLV the pass also writes the beta-x table of its points (phix, see glv_phix).
+template <int C, bool GLV>
+__global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scalars, uint32_t n, int mont_in,
                                                      uint32_t nblk, uint32_t* __restrict__ bcnt,
-                                                     uint32_t* __restrict__ err) {
-  constexpr int W = num_windows<C, NB>(), LOGB = C - 1;
-  constexpr int CB = coarse_bits(C, NB), FB = LOGB - CB, NBIN = 1 << CB;
+                                                     uint32_t* __restrict__ err, const G1Aff* __restrict__ bases,
+                                                     uint4* __restrict__ phix) {
+  using D = Digits<C, GLV>;
+  constexpr int W = D::W, LOGB = C - 1;
+  constexpr int CB = coarse_bits(C, D::NB), FB = LOGB - CB, NBIN = 1 << CB;
   __shared__ uint32_t h[W * NBIN];
   for (int k = threadIdx.x; k < W * NBIN; k += kBlock) h[k] = 0;
   __syncthreads();
-  constexpr uint32_t CH = sort_chunk(C, NB);
+  constexpr uint32_t CH = sort_chunk(D::EP);
   const uint32_t lo = blockIdx.x * CH, hi = min(n, lo + CH);
   for (uint32_t i = lo + threadIdx.x; i < hi; i += kBlock) {
-    uint32_t sgn;
-    const Fr s = load_digits_src<NB>(scalars, i, mont_in, err, sgn);
-    for_each_digit<C, NB>(s, [&](int w, uint32_t mag, uint32_t) {
+    if constexpr (GLV) glv_phix(bases, i, phix);
+    D d;
+    d.load(scalars, i, mont_in, err);
+    d.each([&](int w, uint32_t mag, uint32_t, uint32_t) {
       if (mag) atomicAdd(&h[w * NBIN + ((mag - 1) >> FB)], 1u);
     });
   }
@@ -314,33 +367,34 @@ __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __restrict__ 
 }
 
 // Pass 3: the block's entries are first placed in LDS grouped by (window, bin), then each group
-// is copied to its global run with consecutive lanes writing consecutive addresses.
-template <int C, int NB>
-__global__ void __launch_bounds__(kBlock) k_bin_scatter(const void* __restrict__ scalars, uint32_t n, int mont_in,
+// is copied to its global run with consecutive lanes writing consecutive addresses.  Entry point
+// index: the virtual point (i, or n + i for a GLV k2 digit).
+template <int C, bool GLV>
+__global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ scalars, uint32_t n, int mont_in,
                                                         uint32_t nblk, const uint32_t* __restrict__ bcnt,
                                                         const uint32_t* __restrict__ bstart,
-                                                        uint64_t* __restrict__ tmp) {
-  constexpr int W = num_windows<C, NB>(), LOGB = C - 1;
-  constexpr int CB = coarse_bits(C, NB), FB = LOGB - CB, NBIN = 1 << CB, NK = W * NBIN;
-  // staged entry: local point (9 bits) | sign << 9 | fine << 10 | (window, bin) key << (10 + FB)
-  static_assert(10 + FB + ceil_log2(NK) <= 32, "staged entry overflows 32 bits");
+                                                        uint64_t* __restrict__ tmp, int e32) {
+  using D = Digits<C, GLV>;
+  constexpr int W = D::W, LOGB = C - 1;
+  constexpr int CB = coarse_bits(C, D::NB), FB = LOGB - CB, NBIN = 1 << CB, NK = W * NBIN;
+  // staged entry: local point (9 bits) | half << 9 | sign << 10 | fine << 11 | (window, bin) key << (11 + FB)
+  static_assert(11 + FB + ceil_log2(NK) <= 32, "staged entry overflows 32 bits");
   constexpr uint32_t FMASK = (1u << FB) - 1;
-  constexpr uint32_t CH = sort_chunk(C, NB), PT = CH / kBlock;
+  constexpr uint32_t CH = sort_chunk(D::EP), PT = CH / kBlock;
   __shared__ uint32_t off[NK];   // local group offsets
   __shared__ uint32_t cur[NK];   // cursors
   __shared__ uint32_t part[kBlock];
-  __shared__ uint32_t stage[CH * W];  // see the layout above (no separate key array: 3 blocks per CU)
+  __shared__ uint32_t stage[CH * D::EP];  // see the layout above (no separate key array: 3 blocks per CU)
   const uint32_t blk = blockIdx.x, lo = blk * CH, hi = min(n, lo + CH);
   for (int k = threadIdx.x; k < NK; k += kBlock) off[k] = 0;
   __syncthreads();
-  Fr sc[PT];
-  uint32_t sg[PT];
+  D dg[PT];
 #pragma unroll
   for (int j = 0; j < (int)PT; j++) {
     const uint32_t i = lo + threadIdx.x + j * kBlock;
     if (i < hi) {
-      sc[j] = load_digits_src<NB>(scalars, i, mont_in, nullptr, sg[j]);
-      for_each_digit<C, NB>(sc[j], [&](int w, uint32_t mag, uint32_t) {
+      dg[j].load(scalars, i, mont_in, nullptr);
+      dg[j].each([&](int w, uint32_t mag, uint32_t, uint32_t) {
         if (mag) atomicAdd(&off[w * NBIN + ((mag - 1) >> FB)], 1u);
       });
     }
@@ -353,12 +407,12 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const void* __restrict__
   for (int j = 0; j < (int)PT; j++) {
     const uint32_t li = threadIdx.x + j * kBlock;
     if (lo + li < hi) {
-      for_each_digit<C, NB>(sc[j], [&](int w, uint32_t mag, uint32_t neg) {
+      dg[j].each([&](int w, uint32_t mag, uint32_t neg, uint32_t half) {
         if (mag) {
           const uint32_t b = mag - 1;
           const uint32_t k = w * NBIN + (b >> FB);
           const uint32_t pos = atomicAdd(&cur[k], 1u);
-          stage[pos] = li | ((neg ^ sg[j]) << 9) | ((b & FMASK) << 10) | (k << (10 + FB));
+          stage[pos] = li | (half << 9) | (neg << 10) | ((b & FMASK) << 11) | (k << (11 + FB));
         }
       });
     }
@@ -369,7 +423,10 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const void* __restrict__
   __syncthreads();
   for (uint32_t x = threadIdx.x; x < total; x += kBlock) {
     const uint32_t e = stage[x];
-    tmp[cur[e >> (10 + FB)] + x] = ((uint64_t)((e >> 10) & FMASK) << 32) | (lo + (e & 511u)) | (((e >> 9) & 1u) << 31);
+    const uint32_t pt = lo + (e & 511u) + (((e >> 9) & 1u) ? n : 0u);
+    const uint32_t dst = cur[e >> (11 + FB)] + x, fine = (e >> 11) & FMASK, neg = (e >> 10) & 1u;
+    if (e32) reinterpret_cast<uint32_t*>(tmp)[dst] = pack_entry32(fine, neg, pt, FB);
+    else tmp[dst] = ((uint64_t)fine << 32) | pt | (neg << 31);
   }
 }
 
@@ -386,7 +443,7 @@ static constexpr uint32_t kFineCap = 1024 * kFineR;    // region entries staged 
 static constexpr uint32_t kChunkR = 12, kChunk = 1024 * kChunkR;  // large regions: LDS chunk
 static constexpr size_t kFineLds = (512 + 1024 + (size_t)kFineCap) * 4;  // 78 KiB: 2 blocks per CU
 template <bool BIG>
-__global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__ tmp,
+__global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__ tmp, int e32,
                                                     const uint32_t* __restrict__ bstart, uint32_t FB, uint32_t K,
                                                     uint32_t* __restrict__ gst, uint32_t* __restrict__ tstart,
                                                     uint32_t* __restrict__ ent) {
@@ -405,7 +462,7 @@ __global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__
 #pragma unroll
     for (uint32_t r = 0; r < kFineR; r++) {
       const uint32_t i = tid + r * 1024;
-      x[r] = i < len ? tmp[s0 + i] : 0;
+      x[r] = i < len ? load_entry(tmp, s0 + i, e32, FB) : 0;
     }
 #pragma unroll
     for (uint32_t r = 0; r < kFineR; r++)
@@ -413,14 +470,16 @@ __global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__
   } else {
     uint32_t e = s0 + tid;
     for (; e + 3 * 1024 < s1; e += 4 * 1024) {  // 4 loads in flight per thread
-      const uint32_t f0 = (uint32_t)(tmp[e] >> 32), f1 = (uint32_t)(tmp[e + 1024] >> 32);
-      const uint32_t f2 = (uint32_t)(tmp[e + 2048] >> 32), f3 = (uint32_t)(tmp[e + 3072] >> 32);
+      const uint32_t f0 = (uint32_t)(load_entry(tmp, e, e32, FB) >> 32);
+      const uint32_t f1 = (uint32_t)(load_entry(tmp, e + 1024, e32, FB) >> 32);
+      const uint32_t f2 = (uint32_t)(load_entry(tmp, e + 2048, e32, FB) >> 32);
+      const uint32_t f3 = (uint32_t)(load_entry(tmp, e + 3072, e32, FB) >> 32);
       atomicAdd(&fc[f0], 1u);
       atomicAdd(&fc[f1], 1u);
       atomicAdd(&fc[f2], 1u);
       atomicAdd(&fc[f3], 1u);
     }
-    for (; e < s1; e += 1024) atomicAdd(&fc[(uint32_t)(tmp[e] >> 32)], 1u);
+    for (; e < s1; e += 1024) atomicAdd(&fc[(uint32_t)(load_entry(tmp, e, e32, FB) >> 32)], 1u);
   }
   __syncthreads();
   // exclusive scan of fc[0 .. NF) (NF <= 512)
@@ -460,7 +519,7 @@ __global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__
 #pragma unroll
     for (uint32_t r = 0; r < kChunkR; r++) {
       const uint32_t i = tid + r * 1024;
-      x[r] = i < clen ? tmp[c0 + i] : 0;
+      x[r] = i < clen ? load_entry(tmp, c0 + i, e32, FB) : 0;
       if (i < clen) atomicAdd(&lc[(uint32_t)(x[r] >> 32)], 1u);
     }
     __syncthreads();
@@ -528,7 +587,7 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
     const uint32_t* __restrict__ tstart, uint32_t nbt, uint32_t K, uint32_t T,
     G1Xyzz* __restrict__ bsum, G1Xyzz* __restrict__ pfirst, G1Xyzz* __restrict__ plast,
     uint32_t* __restrict__ multi, uint32_t* __restrict__ nmulti, uint32_t* __restrict__ heavy,
-    uint32_t* __restrict__ nheavy, const G1Aff* __restrict__ phi, uint32_t nsplit) {
+    uint32_t* __restrict__ nheavy, const uint4* __restrict__ phix, uint32_t nsplit) {
   __shared__ G1Xyzz shead[kBlock];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t m = gst[nbt];
@@ -552,7 +611,7 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
     G1Aff pnext;
     {
       const uint32_t idx = vnext & 0x7fffffffu;
-      pnext = load_aff(idx >= nsplit ? phi + (idx - nsplit) : bases + idx, 0);
+      pnext = load_vpoint(bases, phix, idx, nsplit);
     }
 #endif
     for (uint32_t e = s0; e < e_end; e++) {
@@ -575,19 +634,18 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
       }
 #if SV_ACC_PREFETCH == 0
       const uint32_t v = ent[e], idx = v & 0x7fffffffu;
-      // virtual point idx: P_idx, or phi(P_(idx - n)) for the GLV halves (nsplit = n; ~0u without GLV)
-      G1Aff p = load_aff(idx >= nsplit ? phi + (idx - nsplit) : bases + idx, 0);
+      G1Aff p = load_vpoint(bases, phix, idx, nsplit);
 #elif SV_ACC_PREFETCH == 1
       const uint32_t v = vnext, idx = v & 0x7fffffffu;
       if (e + 1 < e_end) vnext = ent[e + 1];
-      G1Aff p = load_aff(idx >= nsplit ? phi + (idx - nsplit) : bases + idx, 0);
+      G1Aff p = load_vpoint(bases, phix, idx, nsplit);
 #else
       const uint32_t v = vnext;
       G1Aff p = pnext;
       if (e + 1 < e_end) {  // next entry's point in flight during this addition
         vnext = ent[e + 1];
         const uint32_t idx = vnext & 0x7fffffffu;
-        pnext = load_aff(idx >= nsplit ? phi + (idx - nsplit) : bases + idx, 0);
+        pnext = load_vpoint(bases, phix, idx, nsplit);
       }
 #endif
       if (v & 0x80000000u) p.y = -p.y;
@@ -731,17 +789,22 @@ __global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, c
   if (tot_out) store_xyzz(tot_out, tid, xyzz_canon2p(run));
 }
 
-// Step 2 fused: one 512-thread block per (window, group) sums the group's H members (strided,
-// ~H/512 serial adds per thread) and finishes with an LDS tree (9 levels) -> out[w*NG + q].
+// Step 2 fused: P 512-thread blocks per (window, group) each sum a 1/P slice of the group's H
+// members (strided, ~H/(512 P) serial adds per thread) and finish with an LDS tree (9 levels).
+// With P > 1 the slices' sums go to part[] and the block that finishes last (device-scope counter
+// cnt[gid], zeroed per call) adds them -> out[w*NG + q].  P = 2 whenever the groups alone would not
+// give every CU a block (GLV at 2^20: 120 groups, 17 -> 13 dependent additions per chain).
 static constexpr int kGroupBlock = 512;
 __global__ void __launch_bounds__(kGroupBlock) k_group_sum(const G1Xyzz* __restrict__ acc,
                                                            const G1Xyzz* __restrict__ tot, uint32_t J,
-                                                           uint32_t logJ, G1Xyzz* __restrict__ out) {
+                                                           uint32_t logJ, uint32_t P, G1Xyzz* __restrict__ out,
+                                                           G1Xyzz* __restrict__ part, uint32_t* __restrict__ cnt) {
   __shared__ G1Xyzz sh[kGroupBlock];
   const uint32_t NG = 2 + logJ, H = J / 2;
-  const uint32_t gid = blockIdx.x, w = gid / NG, q = gid % NG, tid = threadIdx.x;
+  const uint32_t gid = blockIdx.x / P, pp = blockIdx.x % P, w = gid / NG, q = gid % NG, tid = threadIdx.x;
+  const uint32_t m0 = (uint32_t)((uint64_t)H * pp / P), m1 = (uint32_t)((uint64_t)H * (pp + 1) / P);
   G1Xyzz s = G1Xyzz::identity();
-  for (uint32_t m = tid; m < H; m += kGroupBlock) {
+  for (uint32_t m = m0 + tid; m < m1; m += kGroupBlock) {
     G1Xyzz x;
     if (q < 2) {
       x = load_xyzz(acc, w * J + q * H + m);
@@ -758,7 +821,17 @@ __global__ void __launch_bounds__(kGroupBlock) k_group_sum(const G1Xyzz* __restr
     if (tid < st) sh[tid] = xyzz_add_2p(sh[tid], sh[tid + st]);
     __syncthreads();
   }
-  if (tid == 0) store_xyzz(out, gid, xyzz_canon2p(sh[0]));
+  if (tid != 0) return;
+  G1Xyzz v = sh[0];
+  if (P > 1) {
+    store_xyzz(part, blockIdx.x, v);
+    __threadfence();
+    if (atomicAdd(&cnt[gid], 1u) != P - 1) return;
+    __threadfence();
+    for (uint32_t k = 0; k < P; k++)
+      if (k != pp) v = xyzz_add_2p(v, load_xyzz(part, gid * P + k));
+  }
+  store_xyzz(out, gid, xyzz_canon2p(v));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -773,16 +846,20 @@ int msm_last_stats(sv_msm_stats* out) {
 
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
-MsmPlan msm_plan(size_t n) {
+MsmPlan msm_plan(size_t n, bool pieced) {
   MsmPlan p;
-  // GLV (k P = k1 P + k2 phi(P), 128-bit halves) halves the buckets, the bucket reduction and the
-  // Horner chain for the same number of bucket entries, but costs the split, a stored phi(P) table
-  // and a slower sort; measured at 2^20 it lost overall (tail work is not what bounds the tail at
-  // one wave per SIMD) and at 2^24 the doubled table slowed the fill (31 -> 36 ms).  Kept behind
-  // SVGPU_GLV / SVGPU_GLV_MAX_LOG (tests run it both ways).
-  int glv_max_log = 0;  // off by default: measured slower at 2^20 (2.38 vs 2.33 ms; the split + phi table cost more than the halved tail)
+  // GLV (k P = k1 P + k2 phi(P), 128-bit halves, split on the fly by the sort passes) halves the
+  // buckets, the bucket reduction and the host Horner for the same number of bucket entries, at the
+  // cost of a 32-B beta-x table per point.  Measured (r02, med ms, GLV off -> on): 2^14 0.79 -> 0.74,
+  // 2^16 0.98 -> 0.82, 2^18 1.75 -> 1.54, 2^20 2.11 -> 2.05, 2^21 3.74 -> 3.62; at 2^22 (6.88 ->
+  // 7.39) and 2^24 (27.3 -> 31.1) the larger gather working set (bases + beta-x beyond the 256 MiB
+  // Infinity Cache) slows the fill, so it is on up to 2^SVGPU_GLV_MAX_LOG points (default 21);
+  // SVGPU_GLV forces it.
+  int glv_max_log = 21;
   if (const char* e = getenv("SVGPU_GLV_MAX_LOG")) glv_max_log = atoi(e);
-  p.glv = n >= (size_t(1) << 14) && n <= (size_t(1) << glv_max_log);
+  // (pieced: host-fed input streamed in pieces, whose sort + accumulate overlap the transfer; the
+  // GLV split needs every base first, so it stays off there unless forced)
+  p.glv = !pieced && n >= (size_t(1) << 14) && n <= (size_t(1) << glv_max_log);
   if (const char* e = getenv("SVGPU_GLV")) p.glv = atoi(e) != 0 && n >= 2;
   p.npts = p.glv ? 2 * n : n;
   const int nb = p.glv ? 128 : 255;
@@ -811,7 +888,9 @@ MsmPlan msm_plan(size_t n) {
   p.K = (uint32_t)K;
   p.T = cdiv(entries, p.K);
   // reduction: J running-sum segments per window, NG subset groups of H = J/2 points
-  p.logL = 3;  // 8 buckets per running-sum segment (swept: tools/gpu_sweep_red.sh)
+  // 8 buckets per running-sum segment (swept: tools/gpu_sweep_red.sh); 4 with GLV, whose W / 2
+  // windows would otherwise leave half the SIMDs without a k_wsum wave
+  p.logL = p.glv ? 2 : 3;
   if (const char* e = getenv("SVGPU_RED_LOG")) p.logL = atoi(e);
   if (p.logL < 1) p.logL = 1;
   if (p.logL > p.c - 3) p.logL = p.c - 3 > 1 ? p.c - 3 : 1;
@@ -840,29 +919,29 @@ MsmPlan msm_plan(size_t n) {
     default: break;                                                            \
   }
 
-#define SV_LAUNCH_C1(KERNEL, NB, C, GRID, BLOCK, ...)                                              \
+#define SV_LAUNCH_C1(KERNEL, G, C, GRID, BLOCK, ...)                                              \
   switch (C) {                                                                                   \
-    case 4: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<4, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
-    case 5: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<5, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
-    case 6: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<6, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
-    case 7: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<7, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
-    case 8: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<8, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
-    case 9: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<9, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
-    case 10: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<10, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
-    case 11: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<11, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
-    case 12: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<12, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
-    case 13: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<13, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
-    case 14: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<14, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
-    case 15: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<15, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
-    case 16: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<16, NB>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 4: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<4, G>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 5: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<5, G>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 6: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<6, G>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 7: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<7, G>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 8: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<8, G>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 9: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<9, G>), GRID, BLOCK, 0, st, __VA_ARGS__); break;   \
+    case 10: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<10, G>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 11: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<11, G>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 12: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<12, G>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 13: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<13, G>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 14: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<14, G>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 15: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<15, G>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
+    case 16: hipLaunchKernelGGL(HIP_KERNEL_NAME(KERNEL<16, G>), GRID, BLOCK, 0, st, __VA_ARGS__); break; \
     default: break;                                                                              \
   }
-// full scalars (NB = 255) or GLV halves (NB = 128)
+// full scalars or GLV halves (split on the fly)
 #define SV_LAUNCH_C(KERNEL, GLV, C, GRID, BLOCK, ...)              \
   if (GLV) {                                                       \
-    SV_LAUNCH_C1(KERNEL, 128, C, GRID, BLOCK, __VA_ARGS__)         \
+    SV_LAUNCH_C1(KERNEL, true, C, GRID, BLOCK, __VA_ARGS__)        \
   } else {                                                         \
-    SV_LAUNCH_C1(KERNEL, 255, C, GRID, BLOCK, __VA_ARGS__)         \
+    SV_LAUNCH_C1(KERNEL, false, C, GRID, BLOCK, __VA_ARGS__)       \
   }
 
 // Host Horner over (window, group) terms: total = sum_w 2^(c w) [A_lo + A_hi + 2^logL sum_k 2^k U_k]
@@ -896,24 +975,30 @@ struct MsmScratch {
   G1Xyzz *pfirst, *plast;
 };
 
-static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, const void* dsrc, size_t m,
-                     int mont_in, int device, hipStream_t st, G1Xyzz* bsum, const G1Aff* phi, uint32_t nsplit,
+static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, const Fr* scalars, size_t m,
+                     int mont_in, int device, hipStream_t st, G1Xyzz* bsum, const uint4* phix, uint32_t nsplit,
                      hipEvent_t ev_sorted, hipEvent_t ev_sort_mid, hipEvent_t ev_acc_done, hipEvent_t ev_fix_mid,
                      hipEvent_t bases_ready, const G1Aff* conv_src) {
   const int LOGB = p.c - 1;
   const int nb = p.glv ? 128 : 255;
   const uint32_t CB = (uint32_t)coarse_bits(p.c, nb), FB = (uint32_t)LOGB - CB, NBIN = 1u << CB;
   const uint32_t nwb = p.W * NBIN;
-  const uint32_t npts = (uint32_t)m;
-  const uint32_t nblk = cdiv(npts, sort_chunk(p.c, nb));
-  const uint32_t T = cdiv((uint64_t)npts * p.W, p.K);
-  SV_LAUNCH_C(k_bin_hist, p.glv, p.c, dim3(nblk), dim3(kBlock), dsrc, npts, mont_in, nblk, w.bcnt, w.err);
+  const uint32_t npts = (uint32_t)m;  // real points (GLV: 2 m virtual ones)
+  const uint32_t ep = p.glv ? 2 * p.W : p.W;
+  const uint32_t nblk = cdiv(npts, sort_chunk((int)ep));
+  const uint32_t T = cdiv((uint64_t)npts * ep, p.K);
+  // u32 entries when every virtual point index (below nsplit + m with GLV, m without) fits
+  const uint64_t vmax = p.glv ? (uint64_t)nsplit + npts : (uint64_t)npts;
+  int e32 = vmax <= (uint64_t(1) << (31 - FB)) ? 1 : 0;
+  if (const char* e = getenv("SVGPU_SORT_E32")) e32 = e32 && atoi(e) != 0;
+  SV_LAUNCH_C(k_bin_hist, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.err, bases,
+              const_cast<uint4*>(phix));
   SV_HIP(hipGetLastError());
   if (ev_sort_mid) SV_HIP(hipEventRecord(ev_sort_mid, st));
   hipLaunchKernelGGL(k_bin_scan_chunks, dim3(nwb), dim3(kBlock), 0, st, w.bcnt, nblk, w.btot);
   hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, w.btot, nwb, w.bstart, w.gst + p.nbt);
-  SV_LAUNCH_C(k_bin_scatter, p.glv, p.c, dim3(nblk), dim3(kBlock), dsrc, npts, mont_in, nblk, w.bcnt, w.bstart,
-              w.tmp);
+  SV_LAUNCH_C(k_bin_scatter, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.bstart,
+              w.tmp, e32);
   static thread_local int fine_attr_dev = -1;  // the > 64 KiB dynamic-LDS opt-in, once per thread/device
   if (fine_attr_dev != device) {
     SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort<false>),
@@ -922,9 +1007,9 @@ static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, 
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFineLds));
     fine_attr_dev = device;
   }
-  hipLaunchKernelGGL(k_fine_sort<false>, dim3(nwb), dim3(1024), kFineLds, st, w.tmp, w.bstart, FB, p.K, w.gst,
+  hipLaunchKernelGGL(k_fine_sort<false>, dim3(nwb), dim3(1024), kFineLds, st, w.tmp, e32, w.bstart, FB, p.K, w.gst,
                      w.tstart, w.ent);
-  hipLaunchKernelGGL(k_fine_sort<true>, dim3(nwb), dim3(1024), kFineLds, st, w.tmp, w.bstart, FB, p.K, w.gst,
+  hipLaunchKernelGGL(k_fine_sort<true>, dim3(nwb), dim3(1024), kFineLds, st, w.tmp, e32, w.bstart, FB, p.K, w.gst,
                      w.tstart, w.ent);
   SV_HIP(hipGetLastError());
   if (bases_ready) SV_HIP(hipStreamWaitEvent(st, bases_ready, 0));
@@ -933,7 +1018,7 @@ static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, 
                        const_cast<G1Aff*>(bases), npts, w.err);
   if (ev_sorted) SV_HIP(hipEventRecord(ev_sorted, st));
   hipLaunchKernelGGL(k_accumulate, dim3(cdiv(T, kBlock)), dim3(kBlock), 0, st, bases, w.ent, w.gst, w.tstart,
-                     p.nbt, p.K, T, bsum, w.pfirst, w.plast, w.multi, w.nmulti, w.heavy, w.nheavy, phi, nsplit);
+                     p.nbt, p.K, T, bsum, w.pfirst, w.plast, w.multi, w.nmulti, w.heavy, w.nheavy, phix, nsplit);
   SV_HIP(hipGetLastError());
   if (ev_acc_done) SV_HIP(hipEventRecord(ev_acc_done, st));
   hipLaunchKernelGGL(k_fixup_multi, dim3(std::min<uint32_t>(cdiv(p.nbt, kBlock), 1024)), dim3(kBlock), 0, st,
@@ -963,16 +1048,18 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   if (!lease.ok()) return SV_ERR_DEVICE;
   Workspace* ws = lease.get();
   hipStream_t st = ws->stream;
-  MsmPlan p = msm_plan(n);
   // host-fed inputs arrive in pieces: piece k's sort + accumulate run while piece k + 1 is in flight
   int pieces = 1;
   if (feed) {
     pieces = feed->pieces < 1 ? 1 : feed->pieces;
-    if (p.glv || n < (size_t)pieces * 4096) pieces = 1;
+    if (n < (size_t)pieces * 4096) pieces = 1;
     if (pieces > 8) pieces = 8;
   }
+  MsmPlan p = msm_plan(n, pieces > 1);
+  if (p.glv) pieces = 1;
   const size_t max_piece = (n + pieces - 1) / pieces;
-  const uint64_t entries = (uint64_t)(p.glv ? 2 * n : max_piece) * p.W;  // per piece
+  const uint32_t ep = p.glv ? 2 * p.W : p.W;  // entries per real point
+  const uint64_t entries = (uint64_t)max_piece * ep;  // per piece
   const uint32_t Tmax = cdiv(entries, p.K);
 
   // ---- workspace layout (sort / accumulate scratch sized for the largest piece)
@@ -981,14 +1068,18 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   const uint32_t CB = (uint32_t)coarse_bits(p.c, nb), NBIN = 1u << CB;
   (void)LOGB;
   const uint32_t nwb = p.W * NBIN;
-  const uint32_t nblk = cdiv(p.glv ? 2 * n : max_piece, sort_chunk(p.c, nb));
+  const uint32_t nblk = cdiv(max_piece, sort_chunk((int)ep));
   size_t bytes = 0;
   auto add = [&](size_t b) { bytes += Workspace::aligned(b); };
   const bool conv = (form == SV_CANONICAL);
   if (conv) add(n * sizeof(G1Aff));
-  if (p.glv) add(2 * n * sizeof(uint4));      // GLV scalar halves
-  if (p.glv) add(n * sizeof(G1Aff));          // phi(P)
-  add(256);                                   // err flag + heavy/multi queue counters
+  if (p.glv) add(n * 2 * sizeof(uint4));      // GLV: beta x per point
+  const size_t nfinal = (size_t)p.W * p.NG;
+  uint32_t gparts = nfinal < 256 ? 2 : 1;      // k_group_sum blocks per group (see there)
+  if (const char* e = getenv("SVGPU_GROUP_P")) gparts = (uint32_t)std::max(1, atoi(e));
+  if (gparts > p.J / 2) gparts = p.J / 2;
+  const size_t nerr = 64 + nfinal;             // err flag, heavy/multi queue counters, group counters
+  add(nerr * 4);
   add((size_t)nwb * nblk * 4);                // bcnt
   add((size_t)nwb * 4);                       // btot
   add(((size_t)nwb + 1) * 4);                 // bstart
@@ -1004,9 +1095,9 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
     add((size_t)p.nbt * sizeof(G1Xyzz));      // bsum of pieces 1..
     add(((size_t)p.nbt + 1) * 4);             // gst of piece 0
   }
-  const size_t nfinal = (size_t)p.W * p.NG;
   add((size_t)p.J * p.W * sizeof(G1Xyzz) * 2);  // acc_j, T_j
   add(nfinal * sizeof(G1Xyzz));                 // group sums
+  add(nfinal * gparts * sizeof(G1Xyzz));        // group slice sums
   SV_TRY(ws->reserve(bytes));
   SV_TRY(ws->reserve_pinned(nfinal * sizeof(G1Xyzz) + 256));
   if (feed) {
@@ -1020,10 +1111,9 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   const Fr* scalars = reinterpret_cast<const Fr*>(d_scalars);
   const int mont_in = form == SV_MONTGOMERY ? 1 : 0;
   G1Aff* bases_m = conv ? ws->carve<G1Aff>(n) : nullptr;
-  uint4* hs = p.glv ? ws->carve<uint4>(2 * n) : nullptr;
-  G1Aff* phi = p.glv ? ws->carve<G1Aff>(n) : nullptr;
+  uint4* phix = p.glv ? ws->carve<uint4>(2 * n) : nullptr;
   MsmScratch w;
-  w.err = ws->carve<uint32_t>(64);
+  w.err = ws->carve<uint32_t>(nerr);
   w.bcnt = ws->carve<uint32_t>((size_t)nwb * nblk);
   w.btot = ws->carve<uint32_t>(nwb);
   w.bstart = ws->carve<uint32_t>((size_t)nwb + 1);
@@ -1043,13 +1133,18 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   G1Xyzz* racc = ws->carve<G1Xyzz>((size_t)p.J * p.W);
   G1Xyzz* rtot = ws->carve<G1Xyzz>((size_t)p.J * p.W);
   G1Xyzz* ping = ws->carve<G1Xyzz>(nfinal);
+  G1Xyzz* gpart = ws->carve<G1Xyzz>(nfinal * gparts);
 
   hipEvent_t* ev = ws->ev;
   // each event record between kernels costs ~5.5 us of idle GPU (rocprof trace): the accumulate is
   // always bracketed (bench.py's live roofline), the sort / fixup splits only with SVGPU_MSM_STATS=1
-  static const bool detail = getenv("SVGPU_MSM_STATS") && atoi(getenv("SVGPU_MSM_STATS")) != 0;
-  SV_HIP(hipEventRecord(ev[0], st));
-  SV_HIP(hipMemsetAsync(w.err, 0, 256, st));
+  // SVGPU_MSM_LEAN=1 (read per call): only the accumulate's two events, no sort / reduce split
+  static const bool detail_env = getenv("SVGPU_MSM_STATS") && atoi(getenv("SVGPU_MSM_STATS")) != 0;
+  const char* lean_env = getenv("SVGPU_MSM_LEAN");
+  const bool lean = lean_env && atoi(lean_env) != 0;
+  const bool detail = detail_env && !lean;
+  if (!lean) SV_HIP(hipEventRecord(ev[0], st));
+  SV_HIP(hipMemsetAsync(w.err, 0, nerr * 4, st));
   if (feed && p.glv) {  // the GLV split needs every base and scalar first: one piece, then the device path
     SV_HIP(hipEventRecord(ev[6], st));
     SV_HIP(hipStreamWaitEvent(ws->copy_stream, ev[6], 0));
@@ -1064,13 +1159,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
                          w.err);
       bases = bases_m;
     }
-    const void* dsrc = scalars;  // what the sort passes take digits from
-    if (p.glv) {
-      hipLaunchKernelGGL(k_glv_prep, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, st, bases, scalars, (uint32_t)n,
-                         mont_in, hs, phi, w.err);
-      dsrc = hs;
-    }
-    SV_TRY(msm_front(p, w, bases, dsrc, p.npts, mont_in, device, st, bsum, phi, p.glv ? (uint32_t)n : ~0u, ev[2],
+    SV_TRY(msm_front(p, w, bases, scalars, n, mont_in, device, st, bsum, phix, p.glv ? (uint32_t)n : ~0u, ev[2],
                      detail ? ev[1] : nullptr, ev[3], detail ? ev[4] : nullptr, nullptr, nullptr));
   } else {
     // Piece k: the copy stream stages its scalars, then its bases; the compute stream sorts the
@@ -1108,9 +1197,10 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   // of these occupancy-bound kernels takes nearly as long as the whole -- reduce 0.40 -> 0.67 ms.)
   hipLaunchKernelGGL(k_wsum, dim3(cdiv((uint64_t)p.J * p.W, kBlock)), dim3(kBlock), 0, st, bsum,
                      pieces > 1 ? nullptr : w.gst, p.B, p.J, 1u << p.logL, p.W, 1, racc, rtot);
-  hipLaunchKernelGGL(k_group_sum, dim3(p.NG * p.W), dim3(kGroupBlock), 0, st, racc, rtot, p.J, p.logJ, ping);
+  hipLaunchKernelGGL(k_group_sum, dim3(p.NG * p.W * gparts), dim3(kGroupBlock), 0, st, racc, rtot, p.J, p.logJ,
+                     gparts, ping, gpart, w.err + 64);
   SV_HIP(hipGetLastError());
-  SV_HIP(hipEventRecord(ev[5], st));
+  if (!lean) SV_HIP(hipEventRecord(ev[5], st));
   SV_HIP(hipMemcpyAsync(ws->pinned, ping, nfinal * sizeof(G1Xyzz), hipMemcpyDeviceToHost, st));
   SV_HIP(hipMemcpyAsync(ws->pinned + nfinal * sizeof(G1Xyzz), w.err, 4, hipMemcpyDeviceToHost, st));
   SV_HIP(hipStreamSynchronize(st));
@@ -1136,6 +1226,8 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
     s.fixup_ms = ms;
     (void)hipEventElapsedTime(&ms, ev[4], ev[5]);
     s.reduce_ms = ms;
+  } else if (lean) {
+    s.digits_ms = s.sort_ms = s.fixup_ms = s.reduce_ms = -1.0f;  // not measured
   } else {  // digits folded into sort_ms, fixup into reduce_ms
     s.digits_ms = 0;
     (void)hipEventElapsedTime(&ms, ev[0], ev[2]);
@@ -1147,9 +1239,13 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   // host-fed: "accumulate" spans the first piece's accumulate to the last piece's (transfers included)
   (void)hipEventElapsedTime(&ms, ev[2], ev[3]);
   s.accumulate_ms = ms;
-  (void)hipEventElapsedTime(&ms, ev[0], ev[5]);
   s.host_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
-  s.total_ms = ms + s.host_ms;
+  if (lean) {
+    s.total_ms = -1.0f;
+  } else {
+    (void)hipEventElapsedTime(&ms, ev[0], ev[5]);
+    s.total_ms = ms + s.host_ms;
+  }
   s.window_bits = p.c;
   s.num_windows = p.W;
   s.accumulate_launch_units = cdiv((uint64_t)p.npts * p.W, p.K);

@@ -26,7 +26,7 @@ struct MsmPlan {
   size_t npts;      // virtual points: n, or 2n with GLV
 };
 
-MsmPlan msm_plan(size_t n);
+MsmPlan msm_plan(size_t n, bool pieced = false);
 
 // Device-resident MSM on `device`; result (XYZZ, Montgomery) on the host.
 int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int form, int device,

@@ -63,12 +63,17 @@ __device__ __forceinline__ Fr ld_const(const uint32_t* p) {
   return r;
 }
 
-// The permutation runs in field.hpp's 2p domain: every state word stays in [0, 2r) (r < 2^254 is
-// the Fr modulus), so no product pays its final conditional subtraction.  Bounds (R = 2^256,
-// r < 0.19 R): a product of words below 2r is below (4 r^2 + R r) / R < 1.76 r; an MDS row, a fused
-// sum of three products of words below 2r with constants below r, scans below
-// (6 r^2 + R r) / R < 2.14 r and leaves fe_mul_sum's single subtraction below 1.14 r; adding a
-// constant (< r) wraps at 2r (fe_add2p).  The result is canonicalised at the end.
+// The permutation runs in field.hpp's lazily reduced domain: every state word stays below 2.32 r
+// (r < 2^254 is the Fr modulus, r / R < 0.18905 for R = 2^256), so no product pays its final
+// conditional subtraction.  Bounds: a Montgomery product of x, y is below x y / R + r, so
+//   * pow5 of a word below 2.32 r: x^2 < 2.02 r, x^4 < 1.78 r, x^5 < 1.78 r;
+//   * a t = 3 MDS row, a fused sum of three products of words below 2.32 r with constants below r,
+//     scans below (3 * 2.32 * 0.18905 + 1) r < 2.316 r and is kept as scanned (no subtraction);
+//   * "+ constant" after the S-box wraps at 2r (fe_add2p): 1.78 r + r - 2r < r, else below 2r;
+//   * a partial round's state[i] += col_hat[i-1] * state[0] adds a product below 1.38 r and wraps
+//     at 2r, so it never grows past max(2r, its previous bound).
+// The last full round reduces its rows once (below 1.32 r) and the result is canonicalised.  t = 5
+// rows (two fused sums and an addition) keep fe_mul_sum's subtraction.
 __device__ __forceinline__ Fr pow5(const Fr& x) {
   const Fr x2 = fe_sqr_hp<FrTag, false>(x);
   return fe_mul_lazy(fe_sqr_hp<FrTag, false>(x2), x);
@@ -76,13 +81,13 @@ __device__ __forceinline__ Fr pow5(const Fr& x) {
 
 // One MDS row, sum_j s_j M_ij, as fused sums of up to three products with one Montgomery reduction
 // each (fe_mul_sum): t = 3 is one reduction per row instead of three.
-template <int T>
+template <int T, bool kLazy = (T == 3)>
 __device__ __forceinline__ Fr mds_row(const Fr (&s)[T], const uint32_t* row) {
   constexpr int A = T < 3 ? T : 3;
   Fr x[A], y[A];
 #pragma unroll
   for (int j = 0; j < A; j++) x[j] = s[j], y[j] = ld_const(row + j * 8);
-  Fr acc = fe_mul_sum(x, y);
+  Fr acc = fe_mul_sum<FrTag, A, !kLazy>(x, y);
   if constexpr (T > 3) {
     constexpr int B = T - 3;
     static_assert(B <= 3, "mds_row: t <= 6");
@@ -95,21 +100,21 @@ __device__ __forceinline__ Fr mds_row(const Fr (&s)[T], const uint32_t* row) {
 }
 
 // s <- M s for a dense t x t matrix (rows of fused sums of products)
-template <int T>
+template <int T, bool kLazy = (T == 3)>
 __device__ __forceinline__ void apply_mds(Fr (&s)[T], const uint32_t* m) {
   Fr o[T];
 #pragma unroll
-  for (int i = 0; i < T; i++) o[i] = mds_row<T>(s, m + i * T * 8);
+  for (int i = 0; i < T; i++) o[i] = mds_row<T, kLazy>(s, m + i * T * 8);
 #pragma unroll
   for (int i = 0; i < T; i++) s[i] = o[i];
 }
 
 // full round: s_i <- s_i^5 + c_i (State::sbox_full, poseidon.rs:353-357), then the dense matrix
-template <int T>
+template <int T, bool kLazy = (T == 3)>
 __device__ __forceinline__ void full_round(Fr (&s)[T], const uint32_t* c, const uint32_t* m) {
 #pragma unroll
   for (int i = 0; i < T; i++) s[i] = c ? fe_add2p(pow5(s[i]), ld_const(c + i * 8)) : pow5(s[i]);
-  apply_mds<T>(s, m);
+  apply_mds<T, kLazy>(s, m);
 }
 
 // Poseidon::permutation (poseidon.rs:469-500) without the absorbed inputs: the bare HADES map.
@@ -134,7 +139,7 @@ __device__ __forceinline__ void permute(Fr (&s)[T]) {
   }
   const uint32_t* end = PSpec<T>::end();
   for (int r = 0; r < H - 1; r++) full_round<T>(s, end + r * T * 8, PSpec<T>::mds());
-  full_round<T>(s, nullptr, PSpec<T>::mds());
+  full_round<T, false>(s, nullptr, PSpec<T>::mds());  // rows reduced once: below 1.32 r
 #pragma unroll
   for (int i = 0; i < T; i++) s[i] = fe_canon2p(s[i]);
 }

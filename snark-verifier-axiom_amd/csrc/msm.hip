@@ -61,13 +61,15 @@ __device__ __forceinline__ G1Aff load_aff(const G1Aff* __restrict__ a, uint32_t 
 
 // virtual point idx: P_idx, or phi(P_(idx - nsplit)) = (beta x, y) for a GLV k2 entry (nsplit = n;
 // ~0u without GLV): x from the beta-x table, y from the bases
+// (phi64: the table holds whole phi(P) records, 64 B, one gather per entry)
 __device__ __forceinline__ G1Aff load_vpoint(const G1Aff* __restrict__ bases, const uint4* __restrict__ phix,
-                                             uint32_t idx, uint32_t nsplit) {
+                                             uint32_t idx, uint32_t nsplit, int phi64) {
   const bool ph = idx >= nsplit;
   const uint32_t i = ph ? idx - nsplit : idx;
   const uint4* p = reinterpret_cast<const uint4*>(bases + i);
-  const uint4* px = ph ? phix + 2 * i : p;
-  const uint4 q0 = px[0], q1 = px[1], q2 = p[2], q3 = p[3];
+  const uint4* px = ph ? phix + (phi64 ? 4 : 2) * i : p;
+  const uint4* py = ph && phi64 ? px : p;
+  const uint4 q0 = px[0], q1 = px[1], q2 = py[2], q3 = py[3];
   G1Aff r;
   r.x.v[0] = q0.x; r.x.v[1] = q0.y; r.x.v[2] = q0.z; r.x.v[3] = q0.w;
   r.x.v[4] = q1.x; r.x.v[5] = q1.y; r.x.v[6] = q1.z; r.x.v[7] = q1.w;
@@ -207,7 +209,8 @@ struct Digits {
 
 // GLV: phi(P_i) = (beta x_i, y_i); only beta x_i is stored (phix[i], 32 B, written by k_bin_hist),
 // the accumulate reads y_i from the bases (identity (0, 0) maps to itself).
-__device__ __forceinline__ void glv_phix(const G1Aff* __restrict__ bases, uint32_t i, uint4* __restrict__ phix) {
+__device__ __forceinline__ void glv_phix(const G1Aff* __restrict__ bases, uint32_t i, uint4* __restrict__ phix,
+                                         int phi64) {
   const uint4* b = reinterpret_cast<const uint4*>(bases + i);
   Fq x, beta;
   const uint4 x0 = b[0], x1 = b[1];
@@ -216,8 +219,13 @@ __device__ __forceinline__ void glv_phix(const G1Aff* __restrict__ bases, uint32
 #pragma unroll
   for (int j = 0; j < 8; j++) beta.v[j] = GLV_BETA_MONT[j];
   const Fq bx = x * beta;
-  phix[2 * i] = make_uint4(bx.v[0], bx.v[1], bx.v[2], bx.v[3]);
-  phix[2 * i + 1] = make_uint4(bx.v[4], bx.v[5], bx.v[6], bx.v[7]);
+  uint4* o = phix + (phi64 ? 4 : 2) * i;
+  o[0] = make_uint4(bx.v[0], bx.v[1], bx.v[2], bx.v[3]);
+  o[1] = make_uint4(bx.v[4], bx.v[5], bx.v[6], bx.v[7]);
+  if (phi64) {
+    o[2] = b[2];
+    o[3] = b[3];
+  }
 }
 
 // ---- two-level counting sort of the n * W (point, digit) entries by bucket ------------------
@@ -290,7 +298,7 @@ template <int C, bool GLV>
 __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scalars, uint32_t n, int mont_in,
                                                      uint32_t nblk, uint32_t* __restrict__ bcnt,
                                                      uint32_t* __restrict__ err, const G1Aff* __restrict__ bases,
-                                                     uint4* __restrict__ phix) {
+                                                     uint4* __restrict__ phix, int phi64) {
   using D = Digits<C, GLV>;
   constexpr int W = D::W, LOGB = C - 1;
   constexpr int CB = coarse_bits(C, D::NB), FB = LOGB - CB, NBIN = 1 << CB;
@@ -300,7 +308,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scal
   constexpr uint32_t CH = sort_chunk(D::EP);
   const uint32_t lo = blockIdx.x * CH, hi = min(n, lo + CH);
   for (uint32_t i = lo + threadIdx.x; i < hi; i += kBlock) {
-    if constexpr (GLV) glv_phix(bases, i, phix);
+    if constexpr (GLV) glv_phix(bases, i, phix, phi64);
     D d;
     d.load(scalars, i, mont_in, err);
     d.each([&](int w, uint32_t mag, uint32_t, uint32_t) {
@@ -368,10 +376,13 @@ __global__ void __launch_bounds__(1024) k_bin_scan(const uint32_t* __restrict__ 
 
 // Pass 3: the block's entries are first placed in LDS grouped by (window, bin), then each group
 // is copied to its global run with consecutive lanes writing consecutive addresses.  Entry point
-// index: the virtual point (i, or n + i for a GLV k2 digit).
+// index: the virtual point (i, or n + i for a GLV k2 digit).  The block's own (window, bin) counts
+// are not recounted: they are the differences of consecutive block offsets that k_bin_scan_chunks
+// left in bcnt (btot for the last block), which halves the LDS atomics of the pass.
 template <int C, bool GLV>
 __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ scalars, uint32_t n, int mont_in,
                                                         uint32_t nblk, const uint32_t* __restrict__ bcnt,
+                                                        const uint32_t* __restrict__ btot,
                                                         const uint32_t* __restrict__ bstart,
                                                         uint64_t* __restrict__ tmp, int e32) {
   using D = Digits<C, GLV>;
@@ -386,18 +397,15 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
   __shared__ uint32_t part[kBlock];
   __shared__ uint32_t stage[CH * D::EP];  // see the layout above (no separate key array: 3 blocks per CU)
   const uint32_t blk = blockIdx.x, lo = blk * CH, hi = min(n, lo + CH);
-  for (int k = threadIdx.x; k < NK; k += kBlock) off[k] = 0;
-  __syncthreads();
+  for (int k = threadIdx.x; k < NK; k += kBlock) {
+    const size_t at = (size_t)k * nblk + blk;
+    off[k] = (blk + 1 < nblk ? bcnt[at + 1] : btot[k]) - bcnt[at];
+  }
   D dg[PT];
 #pragma unroll
   for (int j = 0; j < (int)PT; j++) {
     const uint32_t i = lo + threadIdx.x + j * kBlock;
-    if (i < hi) {
-      dg[j].load(scalars, i, mont_in, nullptr);
-      dg[j].each([&](int w, uint32_t mag, uint32_t, uint32_t) {
-        if (mag) atomicAdd(&off[w * NBIN + ((mag - 1) >> FB)], 1u);
-      });
-    }
+    if (i < hi) dg[j].load(scalars, i, mont_in, nullptr);
   }
   __syncthreads();
   const uint32_t total = block_excl_scan<NK>(off, part);
@@ -587,7 +595,7 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
     const uint32_t* __restrict__ tstart, uint32_t nbt, uint32_t K, uint32_t T,
     G1Xyzz* __restrict__ bsum, G1Xyzz* __restrict__ pfirst, G1Xyzz* __restrict__ plast,
     uint32_t* __restrict__ multi, uint32_t* __restrict__ nmulti, uint32_t* __restrict__ heavy,
-    uint32_t* __restrict__ nheavy, const uint4* __restrict__ phix, uint32_t nsplit) {
+    uint32_t* __restrict__ nheavy, const uint4* __restrict__ phix, uint32_t nsplit, int phi64) {
   __shared__ G1Xyzz shead[kBlock];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t m = gst[nbt];
@@ -611,7 +619,7 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
     G1Aff pnext;
     {
       const uint32_t idx = vnext & 0x7fffffffu;
-      pnext = load_vpoint(bases, phix, idx, nsplit);
+      pnext = load_vpoint(bases, phix, idx, nsplit, phi64);
     }
 #endif
     for (uint32_t e = s0; e < e_end; e++) {
@@ -634,18 +642,18 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
       }
 #if SV_ACC_PREFETCH == 0
       const uint32_t v = ent[e], idx = v & 0x7fffffffu;
-      G1Aff p = load_vpoint(bases, phix, idx, nsplit);
+      G1Aff p = load_vpoint(bases, phix, idx, nsplit, phi64);
 #elif SV_ACC_PREFETCH == 1
       const uint32_t v = vnext, idx = v & 0x7fffffffu;
       if (e + 1 < e_end) vnext = ent[e + 1];
-      G1Aff p = load_vpoint(bases, phix, idx, nsplit);
+      G1Aff p = load_vpoint(bases, phix, idx, nsplit, phi64);
 #else
       const uint32_t v = vnext;
       G1Aff p = pnext;
       if (e + 1 < e_end) {  // next entry's point in flight during this addition
         vnext = ent[e + 1];
         const uint32_t idx = vnext & 0x7fffffffu;
-        pnext = load_vpoint(bases, phix, idx, nsplit);
+        pnext = load_vpoint(bases, phix, idx, nsplit, phi64);
       }
 #endif
       if (v & 0x80000000u) p.y = -p.y;
@@ -795,43 +803,77 @@ __global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, c
 // cnt[gid], zeroed per call) adds them -> out[w*NG + q].  P = 2 whenever the groups alone would not
 // give every CU a block (GLV at 2^20: 120 groups, 17 -> 13 dependent additions per chain).
 static constexpr int kGroupBlock = 512;
+// member m of group q of window w (see above)
+__device__ __forceinline__ G1Xyzz group_member(const G1Xyzz* __restrict__ acc, const G1Xyzz* __restrict__ tot,
+                                               uint32_t w, uint32_t q, uint32_t J, uint32_t H, uint32_t m) {
+  if (q < 2) return load_xyzz(acc, w * J + q * H + m);
+  const uint32_t k = q - 2;
+  const uint32_t j = ((m >> k) << (k + 1)) | (1u << k) | (m & ((1u << k) - 1));
+  return load_xyzz(tot, w * J + j);
+}
+// XYZZ value of one lane as 32 dwords: LDS in structure-of-arrays order (dword d of lane t at
+// [d][t], conflict-free), and a wave-level shift down by `off` lanes
+__device__ __forceinline__ void sh_put(uint32_t (*sh)[kGroupBlock], uint32_t t, const G1Xyzz& v) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(&v);
+#pragma unroll
+  for (int k = 0; k < 32; k++) sh[k][t] = d[k];
+}
+__device__ __forceinline__ G1Xyzz sh_get(uint32_t (*sh)[kGroupBlock], uint32_t t) {
+  G1Xyzz v;
+  uint32_t* d = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+  for (int k = 0; k < 32; k++) d[k] = sh[k][t];
+  return v;
+}
+__device__ __forceinline__ G1Xyzz wave_down(const G1Xyzz& v, int off) {
+  G1Xyzz r;
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(&v);
+  uint32_t* o = reinterpret_cast<uint32_t*>(&r);
+#pragma unroll
+  for (int k = 0; k < 32; k++) o[k] = __shfl_down(d[k], off);
+  return r;
+}
 __global__ void __launch_bounds__(kGroupBlock) k_group_sum(const G1Xyzz* __restrict__ acc,
                                                            const G1Xyzz* __restrict__ tot, uint32_t J,
                                                            uint32_t logJ, uint32_t P, G1Xyzz* __restrict__ out,
                                                            G1Xyzz* __restrict__ part, uint32_t* __restrict__ cnt) {
-  __shared__ G1Xyzz sh[kGroupBlock];
+  __shared__ uint32_t sh[32][kGroupBlock];  // 64 KiB
   const uint32_t NG = 2 + logJ, H = J / 2;
   const uint32_t gid = blockIdx.x / P, pp = blockIdx.x % P, w = gid / NG, q = gid % NG, tid = threadIdx.x;
   const uint32_t m0 = (uint32_t)((uint64_t)H * pp / P), m1 = (uint32_t)((uint64_t)H * (pp + 1) / P);
+  // strided members, two loads in flight per addition pair
   G1Xyzz s = G1Xyzz::identity();
-  for (uint32_t m = m0 + tid; m < m1; m += kGroupBlock) {
-    G1Xyzz x;
-    if (q < 2) {
-      x = load_xyzz(acc, w * J + q * H + m);
-    } else {
-      const uint32_t k = q - 2;
-      const uint32_t j = ((m >> k) << (k + 1)) | (1u << k) | (m & ((1u << k) - 1));
-      x = load_xyzz(tot, w * J + j);
-    }
-    s = xyzz_add_2p(s, x);
+  uint32_t m = m0 + tid;
+  for (; m + kGroupBlock < m1; m += 2 * kGroupBlock) {
+    const G1Xyzz x0 = group_member(acc, tot, w, q, J, H, m);
+    const G1Xyzz x1 = group_member(acc, tot, w, q, J, H, m + kGroupBlock);
+    s = xyzz_add_2p(s, x0);
+    s = xyzz_add_2p(s, x1);
   }
-  sh[tid] = s;
-  __syncthreads();
-  for (uint32_t st = kGroupBlock / 2; st > 0; st >>= 1) {
-    if (tid < st) sh[tid] = xyzz_add_2p(sh[tid], sh[tid + st]);
+  if (m < m1) s = xyzz_add_2p(s, group_member(acc, tot, w, q, J, H, m));
+  // tree: three cross-wave levels through LDS, then six inside wave 0
+  for (uint32_t st = kGroupBlock / 2; st >= 64; st >>= 1) {
+    if (tid >= st && tid < 2 * st) sh_put(sh, tid, s);
+    __syncthreads();
+    if (tid < st) s = xyzz_add_2p(s, sh_get(sh, tid + st));
     __syncthreads();
   }
+  if (tid >= 64) return;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const G1Xyzz o = wave_down(s, off);
+    if ((int)tid < off) s = xyzz_add_2p(s, o);
+  }
   if (tid != 0) return;
-  G1Xyzz v = sh[0];
   if (P > 1) {
-    store_xyzz(part, blockIdx.x, v);
+    store_xyzz(part, blockIdx.x, s);
     __threadfence();
     if (atomicAdd(&cnt[gid], 1u) != P - 1) return;
     __threadfence();
     for (uint32_t k = 0; k < P; k++)
-      if (k != pp) v = xyzz_add_2p(v, load_xyzz(part, gid * P + k));
+      if (k != pp) s = xyzz_add_2p(s, load_xyzz(part, gid * P + k));
   }
-  store_xyzz(out, gid, xyzz_canon2p(v));
+  store_xyzz(out, gid, xyzz_canon2p(s));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -862,6 +904,8 @@ MsmPlan msm_plan(size_t n, bool pieced) {
   p.glv = !pieced && n >= (size_t(1) << 14) && n <= (size_t(1) << glv_max_log);
   if (const char* e = getenv("SVGPU_GLV")) p.glv = atoi(e) != 0 && n >= 2;
   p.npts = p.glv ? 2 * n : n;
+  p.phi64 = 0;
+  if (const char* e = getenv("SVGPU_GLV_PHI64")) p.phi64 = atoi(e) != 0;
   const int nb = p.glv ? 128 : 255;
   int lg = 0;
   while ((size_t(1) << (lg + 1)) <= p.npts) lg++;
@@ -944,25 +988,23 @@ MsmPlan msm_plan(size_t n, bool pieced) {
     SV_LAUNCH_C1(KERNEL, false, C, GRID, BLOCK, __VA_ARGS__)       \
   }
 
-// Host Horner over (window, group) terms: total = sum_w 2^(c w) [A_lo + A_hi + 2^logL sum_k 2^k U_k]
-// (k < logJ; J >= 4, so every window has U terms): each window's S_w by its own Horner (27 point
-// operations), then the Horner over windows (c (W - 1) doublings) -- 690 point operations instead
-// of 740 for one Horner over every exponent.  (Running the windows' S_w on the host pool cost more
-// than it saved: waking the pool per MSM, and its spinning workers then slowed the caller's next
-// launches -- 2.27 -> 2.52 ms per step at 2^20.)
+// Host Horner over every exponent: the group sums of window w are A_lo, A_hi at 2^(c w) and U_k at
+// 2^(c w + logL + k), k < logJ (logL + logJ = c - 1, so the windows' exponents never collide), so one
+// chain of c (W - 1) + c - 2 doublings with each term added at its exponent computes the total --
+// 126 doublings + 120 additions with GLV at 2^20 instead of 224 + 119 for a Horner per window
+// followed by one over the windows.
 static host::Xyzz host_combine(const MsmPlan& p, const host::Xyzz* A) {
-  std::vector<host::Xyzz> S(p.W);
-  for (uint32_t w = 0; w < p.W; w++) {
+  const int top = (int)((p.W - 1) * p.c + p.logL + p.logJ - 1);
+  host::Xyzz acc = host::x_identity();
+  for (int e = top; e >= 0; e--) {
+    acc = host::x_dbl(acc);
+    const uint32_t w = (uint32_t)e / p.c, r = (uint32_t)e % p.c;
     const host::Xyzz* a = A + w * p.NG;
-    host::Xyzz acc = a[p.NG - 1];
-    for (int q = (int)p.NG - 2; q >= 2; q--) acc = host::x_add(host::x_dbl(acc), a[q]);
-    for (uint32_t i = 0; i < p.logL; i++) acc = host::x_dbl(acc);
-    S[w] = host::x_add(host::x_add(acc, a[0]), a[1]);
-  }
-  host::Xyzz acc = S[p.W - 1];
-  for (int w = (int)p.W - 2; w >= 0; w--) {
-    for (int i = 0; i < p.c; i++) acc = host::x_dbl(acc);
-    acc = host::x_add(acc, S[w]);
+    if (r == 0) {
+      acc = host::x_add(host::x_add(acc, a[0]), a[1]);
+    } else if (r >= p.logL && r - p.logL < p.logJ) {
+      acc = host::x_add(acc, a[2 + r - p.logL]);
+    }
   }
   return acc;
 }
@@ -978,7 +1020,8 @@ struct MsmScratch {
 static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, const Fr* scalars, size_t m,
                      int mont_in, int device, hipStream_t st, G1Xyzz* bsum, const uint4* phix, uint32_t nsplit,
                      hipEvent_t ev_sorted, hipEvent_t ev_sort_mid, hipEvent_t ev_acc_done, hipEvent_t ev_fix_mid,
-                     hipEvent_t bases_ready, const G1Aff* conv_src) {
+                     hipEvent_t bases_ready, const G1Aff* conv_src, hipStream_t side = nullptr,
+                     hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr) {
   const int LOGB = p.c - 1;
   const int nb = p.glv ? 128 : 255;
   const uint32_t CB = (uint32_t)coarse_bits(p.c, nb), FB = (uint32_t)LOGB - CB, NBIN = 1u << CB;
@@ -992,12 +1035,12 @@ static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, 
   int e32 = vmax <= (uint64_t(1) << (31 - FB)) ? 1 : 0;
   if (const char* e = getenv("SVGPU_SORT_E32")) e32 = e32 && atoi(e) != 0;
   SV_LAUNCH_C(k_bin_hist, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.err, bases,
-              const_cast<uint4*>(phix));
+              const_cast<uint4*>(phix), p.phi64);
   SV_HIP(hipGetLastError());
   if (ev_sort_mid) SV_HIP(hipEventRecord(ev_sort_mid, st));
   hipLaunchKernelGGL(k_bin_scan_chunks, dim3(nwb), dim3(kBlock), 0, st, w.bcnt, nblk, w.btot);
   hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, w.btot, nwb, w.bstart, w.gst + p.nbt);
-  SV_LAUNCH_C(k_bin_scatter, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.bstart,
+  SV_LAUNCH_C(k_bin_scatter, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.btot, w.bstart,
               w.tmp, e32);
   static thread_local int fine_attr_dev = -1;  // the > 64 KiB dynamic-LDS opt-in, once per thread/device
   if (fine_attr_dev != device) {
@@ -1007,10 +1050,21 @@ static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, 
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFineLds));
     fine_attr_dev = device;
   }
+  // the two fine-sort instantiations touch disjoint regions: with a side stream the large-region
+  // one (a few dozen blocks, the top windows' crowded bins) runs concurrently with the other
+  hipStream_t big_st = side ? side : st;
+  if (side) {
+    SV_HIP(hipEventRecord(ev_fork, st));
+    SV_HIP(hipStreamWaitEvent(side, ev_fork, 0));
+  }
+  hipLaunchKernelGGL(k_fine_sort<true>, dim3(nwb), dim3(1024), kFineLds, big_st, w.tmp, e32, w.bstart, FB, p.K,
+                     w.gst, w.tstart, w.ent);
   hipLaunchKernelGGL(k_fine_sort<false>, dim3(nwb), dim3(1024), kFineLds, st, w.tmp, e32, w.bstart, FB, p.K, w.gst,
                      w.tstart, w.ent);
-  hipLaunchKernelGGL(k_fine_sort<true>, dim3(nwb), dim3(1024), kFineLds, st, w.tmp, e32, w.bstart, FB, p.K, w.gst,
-                     w.tstart, w.ent);
+  if (side) {
+    SV_HIP(hipEventRecord(ev_join, side));
+    SV_HIP(hipStreamWaitEvent(st, ev_join, 0));
+  }
   SV_HIP(hipGetLastError());
   if (bases_ready) SV_HIP(hipStreamWaitEvent(st, bases_ready, 0));
   if (conv_src)  // host-fed canonical bases: converted once they have landed, after the sort
@@ -1018,7 +1072,7 @@ static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, 
                        const_cast<G1Aff*>(bases), npts, w.err);
   if (ev_sorted) SV_HIP(hipEventRecord(ev_sorted, st));
   hipLaunchKernelGGL(k_accumulate, dim3(cdiv(T, kBlock)), dim3(kBlock), 0, st, bases, w.ent, w.gst, w.tstart,
-                     p.nbt, p.K, T, bsum, w.pfirst, w.plast, w.multi, w.nmulti, w.heavy, w.nheavy, phix, nsplit);
+                     p.nbt, p.K, T, bsum, w.pfirst, w.plast, w.multi, w.nmulti, w.heavy, w.nheavy, phix, nsplit, p.phi64);
   SV_HIP(hipGetLastError());
   if (ev_acc_done) SV_HIP(hipEventRecord(ev_acc_done, st));
   hipLaunchKernelGGL(k_fixup_multi, dim3(std::min<uint32_t>(cdiv(p.nbt, kBlock), 1024)), dim3(kBlock), 0, st,
@@ -1073,7 +1127,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   auto add = [&](size_t b) { bytes += Workspace::aligned(b); };
   const bool conv = (form == SV_CANONICAL);
   if (conv) add(n * sizeof(G1Aff));
-  if (p.glv) add(n * 2 * sizeof(uint4));      // GLV: beta x per point
+  if (p.glv) add(n * (p.phi64 ? 4 : 2) * sizeof(uint4));  // GLV: beta x (or phi(P)) per point
   const size_t nfinal = (size_t)p.W * p.NG;
   uint32_t gparts = nfinal < 256 ? 2 : 1;      // k_group_sum blocks per group (see there)
   if (const char* e = getenv("SVGPU_GROUP_P")) gparts = (uint32_t)std::max(1, atoi(e));
@@ -1111,9 +1165,11 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   const Fr* scalars = reinterpret_cast<const Fr*>(d_scalars);
   const int mont_in = form == SV_MONTGOMERY ? 1 : 0;
   G1Aff* bases_m = conv ? ws->carve<G1Aff>(n) : nullptr;
-  uint4* phix = p.glv ? ws->carve<uint4>(2 * n) : nullptr;
+  uint4* phix = p.glv ? ws->carve<uint4>((p.phi64 ? 4 : 2) * n) : nullptr;
   MsmScratch w;
-  w.err = ws->carve<uint32_t>(nerr);
+  // the group sums and the error flag / counters share one region: one D2H copy reads both
+  G1Xyzz* ping = ws->carve<G1Xyzz>(nfinal + (nerr * 4 + sizeof(G1Xyzz) - 1) / sizeof(G1Xyzz));
+  w.err = reinterpret_cast<uint32_t*>(ping + nfinal);
   w.bcnt = ws->carve<uint32_t>((size_t)nwb * nblk);
   w.btot = ws->carve<uint32_t>(nwb);
   w.bstart = ws->carve<uint32_t>((size_t)nwb + 1);
@@ -1132,7 +1188,6 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   uint32_t* gst0 = pieces > 1 ? ws->carve<uint32_t>((size_t)p.nbt + 1) : nullptr;
   G1Xyzz* racc = ws->carve<G1Xyzz>((size_t)p.J * p.W);
   G1Xyzz* rtot = ws->carve<G1Xyzz>((size_t)p.J * p.W);
-  G1Xyzz* ping = ws->carve<G1Xyzz>(nfinal);
   G1Xyzz* gpart = ws->carve<G1Xyzz>(nfinal * gparts);
 
   hipEvent_t* ev = ws->ev;
@@ -1143,6 +1198,8 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   const char* lean_env = getenv("SVGPU_MSM_LEAN");
   const bool lean = lean_env && atoi(lean_env) != 0;
   const bool detail = detail_env && !lean;
+  const char* fork_env = getenv("SVGPU_SORT_FORK");
+  const bool fork_sort = fork_env && atoi(fork_env) != 0;  // off: measured slower (the join delays the accumulate)
   if (!lean) SV_HIP(hipEventRecord(ev[0], st));
   SV_HIP(hipMemsetAsync(w.err, 0, nerr * 4, st));
   if (feed && p.glv) {  // the GLV split needs every base and scalar first: one piece, then the device path
@@ -1159,8 +1216,14 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
                          w.err);
       bases = bases_m;
     }
+    hipStream_t side = nullptr;
+    if (fork_sort) {
+      SV_TRY(ws->ensure_copy_stream());  // idle on the device path
+      side = ws->copy_stream;
+    }
     SV_TRY(msm_front(p, w, bases, scalars, n, mont_in, device, st, bsum, phix, p.glv ? (uint32_t)n : ~0u, ev[2],
-                     detail ? ev[1] : nullptr, ev[3], detail ? ev[4] : nullptr, nullptr, nullptr));
+                     detail ? ev[1] : nullptr, ev[3], detail ? ev[4] : nullptr, nullptr, nullptr, side, ev[24],
+                     ev[25]));
   } else {
     // Piece k: the copy stream stages its scalars, then its bases; the compute stream sorts the
     // piece once its scalars have landed and accumulates it once its bases have (k_to_mont_bases
@@ -1201,8 +1264,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
                      gparts, ping, gpart, w.err + 64);
   SV_HIP(hipGetLastError());
   if (!lean) SV_HIP(hipEventRecord(ev[5], st));
-  SV_HIP(hipMemcpyAsync(ws->pinned, ping, nfinal * sizeof(G1Xyzz), hipMemcpyDeviceToHost, st));
-  SV_HIP(hipMemcpyAsync(ws->pinned + nfinal * sizeof(G1Xyzz), w.err, 4, hipMemcpyDeviceToHost, st));
+  SV_HIP(hipMemcpyAsync(ws->pinned, ping, nfinal * sizeof(G1Xyzz) + 4, hipMemcpyDeviceToHost, st));
   SV_HIP(hipStreamSynchronize(st));
   uint32_t errv;
   memcpy(&errv, ws->pinned + nfinal * sizeof(G1Xyzz), 4);

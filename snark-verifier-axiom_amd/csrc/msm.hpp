@@ -24,6 +24,7 @@ struct MsmPlan {
   uint32_t NG;      // subset-sum groups per window: 2 + logJ
   bool glv;         // GLV split: 2n virtual points (P, phi(P)) with 128-bit scalar halves
   size_t npts;      // virtual points: n, or 2n with GLV
+  int phi64;        // GLV table: whole phi(P) records (1) or beta x only (0)
 };
 
 MsmPlan msm_plan(size_t n, bool pieced = false);

@@ -34,7 +34,7 @@ struct Workspace {
   char* stage = nullptr;
   size_t stage_cap = 0;
   hipStream_t copy_stream = nullptr;
-  static constexpr int kEvents = 24;
+  static constexpr int kEvents = 26;
   hipEvent_t ev[kEvents] = {};
 
 

@@ -228,6 +228,12 @@ __device__ __forceinline__ void glv_phix(const G1Aff* __restrict__ bases, uint32
   }
 }
 
+// Host-fed pieces: the piece's table once its bases have landed (its sort ran on the scalars alone)
+__global__ void k_glv_phix(const G1Aff* __restrict__ bases, uint32_t n, uint4* __restrict__ phix, int phi64) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) glv_phix(bases, i, phix, phi64);
+}
+
 // ---- two-level counting sort of the n * W (point, digit) entries by bucket ------------------
 // Bucket b = |digit| - 1 of window w splits into a coarse bin b >> FB (NBIN = 2^CB bins per window)
 // and a fine index b & (2^FB - 1).  Pass 1 (k_bin_hist): per block of sort_chunk(c) points, every
@@ -308,7 +314,9 @@ __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scal
   constexpr uint32_t CH = sort_chunk(D::EP);
   const uint32_t lo = blockIdx.x * CH, hi = min(n, lo + CH);
   for (uint32_t i = lo + threadIdx.x; i < hi; i += kBlock) {
-    if constexpr (GLV) glv_phix(bases, i, phix, phi64);
+    if constexpr (GLV) {
+      if (phix) glv_phix(bases, i, phix, phi64);  // (null: bases not landed yet, k_glv_phix later)
+    }
     D d;
     d.load(scalars, i, mont_in, err);
     d.each([&](int w, uint32_t mag, uint32_t, uint32_t) {
@@ -888,7 +896,7 @@ int msm_last_stats(sv_msm_stats* out) {
 
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
-MsmPlan msm_plan(size_t n, bool pieced) {
+MsmPlan msm_plan(size_t n) {
   MsmPlan p;
   // GLV (k P = k1 P + k2 phi(P), 128-bit halves, split on the fly by the sort passes) halves the
   // buckets, the bucket reduction and the host Horner for the same number of bucket entries, at the
@@ -899,12 +907,13 @@ MsmPlan msm_plan(size_t n, bool pieced) {
   // SVGPU_GLV forces it.
   int glv_max_log = 21;
   if (const char* e = getenv("SVGPU_GLV_MAX_LOG")) glv_max_log = atoi(e);
-  // (pieced: host-fed input streamed in pieces, whose sort + accumulate overlap the transfer; the
-  // GLV split needs every base first, so it stays off there unless forced)
-  p.glv = !pieced && n >= (size_t(1) << 14) && n <= (size_t(1) << glv_max_log);
+  p.glv = n >= (size_t(1) << 14) && n <= (size_t(1) << glv_max_log);
   if (const char* e = getenv("SVGPU_GLV")) p.glv = atoi(e) != 0 && n >= 2;
   p.npts = p.glv ? 2 * n : n;
-  p.phi64 = 0;
+  // whole phi(P) records (one 64-B gather per k2 entry) while bases + table stay well inside the
+  // Infinity Cache; beta-x only above (measured at 2^20: 1.97-2.01 vs 2.01-2.15 ms, k_accumulate
+  // 1.39 vs 1.39-1.50 ms)
+  p.phi64 = n <= (size_t(1) << 20);
   if (const char* e = getenv("SVGPU_GLV_PHI64")) p.phi64 = atoi(e) != 0;
   const int nb = p.glv ? 128 : 255;
   int lg = 0;
@@ -1035,7 +1044,7 @@ static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, 
   int e32 = vmax <= (uint64_t(1) << (31 - FB)) ? 1 : 0;
   if (const char* e = getenv("SVGPU_SORT_E32")) e32 = e32 && atoi(e) != 0;
   SV_LAUNCH_C(k_bin_hist, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.err, bases,
-              const_cast<uint4*>(phix), p.phi64);
+              bases_ready ? nullptr : const_cast<uint4*>(phix), p.phi64);
   SV_HIP(hipGetLastError());
   if (ev_sort_mid) SV_HIP(hipEventRecord(ev_sort_mid, st));
   hipLaunchKernelGGL(k_bin_scan_chunks, dim3(nwb), dim3(kBlock), 0, st, w.bcnt, nblk, w.btot);
@@ -1070,6 +1079,9 @@ static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, 
   if (conv_src)  // host-fed canonical bases: converted once they have landed, after the sort
     hipLaunchKernelGGL(k_to_mont_bases, dim3(cdiv(npts, kBlock)), dim3(kBlock), 0, st, conv_src,
                        const_cast<G1Aff*>(bases), npts, w.err);
+  if (bases_ready && p.glv)  // host-fed GLV piece: its phi table from the landed (converted) bases
+    hipLaunchKernelGGL(k_glv_phix, dim3(cdiv(npts, kBlock)), dim3(kBlock), 0, st, bases, npts,
+                       const_cast<uint4*>(phix), p.phi64);
   if (ev_sorted) SV_HIP(hipEventRecord(ev_sorted, st));
   hipLaunchKernelGGL(k_accumulate, dim3(cdiv(T, kBlock)), dim3(kBlock), 0, st, bases, w.ent, w.gst, w.tstart,
                      p.nbt, p.K, T, bsum, w.pfirst, w.plast, w.multi, w.nmulti, w.heavy, w.nheavy, phix, nsplit, p.phi64);
@@ -1109,8 +1121,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
     if (n < (size_t)pieces * 4096) pieces = 1;
     if (pieces > 8) pieces = 8;
   }
-  MsmPlan p = msm_plan(n, pieces > 1);
-  if (p.glv) pieces = 1;
+  MsmPlan p = msm_plan(n);
   const size_t max_piece = (n + pieces - 1) / pieces;
   const uint32_t ep = p.glv ? 2 * p.W : p.W;  // entries per real point
   const uint64_t entries = (uint64_t)max_piece * ep;  // per piece
@@ -1202,15 +1213,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   const bool fork_sort = fork_env && atoi(fork_env) != 0;  // off: measured slower (the join delays the accumulate)
   if (!lean) SV_HIP(hipEventRecord(ev[0], st));
   SV_HIP(hipMemsetAsync(w.err, 0, nerr * 4, st));
-  if (feed && p.glv) {  // the GLV split needs every base and scalar first: one piece, then the device path
-    SV_HIP(hipEventRecord(ev[6], st));
-    SV_HIP(hipStreamWaitEvent(ws->copy_stream, ev[6], 0));
-    SV_TRY(feed->stage(0, n, const_cast<void*>(d_bases), const_cast<void*>(d_scalars), ws->copy_stream, ws->ev[8],
-                       ws->ev[9]));
-    SV_HIP(hipStreamWaitEvent(st, ws->ev[8], 0));
-    SV_HIP(hipStreamWaitEvent(st, ws->ev[9], 0));
-  }
-  if (!feed || p.glv) {
+  if (!feed) {
     if (conv) {
       hipLaunchKernelGGL(k_to_mont_bases, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, st, bases, bases_m, (uint32_t)n,
                          w.err);
@@ -1241,8 +1244,11 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
       if (k > 0) SV_HIP(hipMemsetAsync(w.err + 1, 0, 8, st));  // fixup queue counters
       const G1Aff* pb = conv ? bases_m + lo : db;
       G1Xyzz* dst = k == 0 ? bsum : bsum_k;
-      SV_TRY(msm_front(p, w, pb, dsc, m, mont_in, device, st, dst, nullptr, ~0u, k == 0 ? ev[2] : nullptr, nullptr,
-                       k == pieces - 1 ? ev[3] : nullptr, nullptr, b_ready, conv ? db : nullptr));
+      // GLV: piece-local virtual points (i, m + i) over the piece's bases and its slice of the table
+      uint4* phix_k = p.glv ? phix + (size_t)(p.phi64 ? 4 : 2) * lo : nullptr;
+      SV_TRY(msm_front(p, w, pb, dsc, m, mont_in, device, st, dst, phix_k, p.glv ? (uint32_t)m : ~0u,
+                       k == 0 ? ev[2] : nullptr, nullptr, k == pieces - 1 ? ev[3] : nullptr, nullptr, b_ready,
+                       conv ? db : nullptr));
       if (pieces > 1) {
         if (k == 0) {
           SV_HIP(hipMemcpyAsync(gst0, w.gst, ((size_t)p.nbt + 1) * 4, hipMemcpyDeviceToDevice, st));

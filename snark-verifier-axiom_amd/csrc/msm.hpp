@@ -27,7 +27,7 @@ struct MsmPlan {
   int phi64;        // GLV table: whole phi(P) records (1) or beta x only (0)
 };
 
-MsmPlan msm_plan(size_t n, bool pieced = false);
+MsmPlan msm_plan(size_t n);
 
 // Device-resident MSM on `device`; result (XYZZ, Montgomery) on the host.
 int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int form, int device,

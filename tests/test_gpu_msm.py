@@ -216,3 +216,18 @@ def test_glv_split_on_off(gpu, oracle_cpp, n, glv, monkeypatch):
         Bm = enc.bases_array(pts, svgpu.SV_MONTGOMERY)
         Sm = enc.scalars_array(sc, svgpu.SV_MONTGOMERY)
         assert svgpu.msm_arrays(Bm, Sm, svgpu.SV_MONTGOMERY) == exp
+
+
+@pytest.mark.parametrize("phi64", ["0", "1"])
+@pytest.mark.parametrize("n", [3, 4097, 65537])
+def test_glv_phi_table_layouts(gpu, oracle_cpp, n, phi64, monkeypatch):
+    """GLV with the beta-x-only table (k2 entries read y from the bases) and with whole phi(P)
+    records (SVGPU_GLV_PHI64), identity bases included, against the reference Pippenger."""
+    import svgpu
+    monkeypatch.setenv("SVGPU_GLV", "1")
+    monkeypatch.setenv("SVGPU_GLV_PHI64", phi64)
+    B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=17 * n)
+    S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=17 * n)
+    B[n // 2] = 0  # identity (0, 0) maps to itself under phi
+    exp = _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
+    assert svgpu.msm_arrays(B, S, svgpu.SV_CANONICAL) == exp

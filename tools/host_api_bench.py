@@ -37,10 +37,13 @@ B = Bd.cpu().numpy().view(np.uint64).copy()
 S = Sd.cpu().numpy().view(np.uint64).copy()
 dms, ref = t(lambda: (dv.msm(Bd, Sd, M), torch.cuda.synchronize())[0])
 print(f"device-resident  {dms:7.3f} ms")
-for p in ("1", "2", "4", "8"):
-    os.environ["SVGPU_H2D_PIECES"] = p
-    ms, r = t(lambda: svgpu.msm_arrays(B, S, M))
-    print(f"host pieces={p}    {ms:7.3f} ms  x{ms / dms:.2f}  ok={r == ref}")
+for glv in ("1", "0"):
+    os.environ["SVGPU_GLV"] = glv
+    for p in ("1", "2", "4", "6", "8"):
+        os.environ["SVGPU_H2D_PIECES"] = p
+        ms, r = t(lambda: svgpu.msm_arrays(B, S, M))
+        print(f"host glv={glv} pieces={p}    {ms:7.3f} ms  x{ms / dms:.2f}  ok={r == ref}")
+os.environ.pop("SVGPU_GLV")
 os.environ["SVGPU_H2D_PIECES"] = "4"
 rng = np.random.default_rng(1)
 perm = rng.permutation(n)

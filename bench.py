@@ -63,13 +63,17 @@ def ref_window(n: int) -> int:
 
 
 def _time(fn, reps):
+    """Median over reps of one synchronised call (latency of the secondary rows; a single host-pool
+    or clock hiccup would otherwise dominate a mean over 5 calls)."""
     fn()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    ts = []
     for _ in range(reps):
+        t0 = time.perf_counter()
         r = fn()
-    torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / reps, r
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), r
 
 
 def next_rows(dev, dv, ob, enc, g2, sg2, accs):

@@ -310,7 +310,7 @@ def main():
             "x_device_resident": h_s * 1e3 / dev_ms,
             "refs_gather_inclusive_ms": r_s * 1e3,
             "refs_x_device_resident": r_s * 1e3 / dev_ms,
-            "h2d_pieces": int(os.environ.get("SVGPU_H2D_PIECES", "4")),
+            "h2d_pieces": os.environ.get("SVGPU_H2D_PIECES", "auto (2 with the GLV split, 4 without)"),
             "same_result_as_device_path": bool(h_res == result and r_res == result),
             "note": "sv_bn254_g1_msm: pageable host arrays -> HBM in pieces on a copy stream, each piece sorted and "
                     "accumulated while the next is in flight (median of 7 calls, transfer included); "

@@ -128,11 +128,12 @@ struct Staging {
   }
 };
 
-// pieces of a host-fed MSM (SVGPU_H2D_PIECES, default 4): piece k + 1's transfer overlaps piece
-// k's sort and accumulation
+// pieces of a host-fed MSM (SVGPU_H2D_PIECES; unset = 0: the MSM plan picks, see msm_run_impl):
+// piece k + 1's transfer overlaps piece k's sort and accumulation
 int h2d_pieces() {
   const char* e = getenv("SVGPU_H2D_PIECES");
-  const int p = e ? atoi(e) : 4;
+  if (!e) return 0;
+  const int p = atoi(e);
   return p < 1 ? 1 : p;
 }
 
@@ -198,13 +199,15 @@ int sv_bn254_g1_msm(const sv_g1_affine* bases, const sv_fe* scalars, size_t n, i
     if (lo >= hi) return SV_OK;
     MsmFeed feed;
     feed.pieces = h2d_pieces();
-    feed.stage = [&, lo](size_t a, size_t b, void* db, void* ds, hipStream_t cs, hipEvent_t sc_ready,
-                         hipEvent_t b_ready) -> int {
-      // pageable caller memory: the runtime's staged DMA measured at the pinned rate (tools/ubench_h2d.cpp)
+    // pageable caller memory: the runtime's staged DMA measured at the pinned rate (tools/ubench_h2d.cpp)
+    feed.stage_scalars = [&, lo](size_t a, size_t b, void* ds, hipStream_t cs, hipEvent_t ready) -> int {
       SV_HIP(hipMemcpyAsync(ds, scalars + lo + a, (b - a) * sizeof(sv_fe), hipMemcpyHostToDevice, cs));
-      SV_HIP(hipEventRecord(sc_ready, cs));
+      SV_HIP(hipEventRecord(ready, cs));
+      return SV_OK;
+    };
+    feed.stage_bases = [&, lo](size_t a, size_t b, void* db, hipStream_t cs, hipEvent_t ready) -> int {
       SV_HIP(hipMemcpyAsync(db, bases + lo + a, (b - a) * sizeof(sv_g1_affine), hipMemcpyHostToDevice, cs));
-      SV_HIP(hipEventRecord(b_ready, cs));
+      SV_HIP(hipEventRecord(ready, cs));
       return SV_OK;
     };
     return msm_run_fed(hi - lo, form, dev, feed, &part[k]);
@@ -250,10 +253,9 @@ int sv_bn254_g1_msm_refs(const sv_msm_ref* pairs, size_t n, int form, int num_gp
     std::atomic<int> null_ref{0};
     MsmFeed feed;
     feed.pieces = h2d_pieces();
-    feed.stage = [&, lo](size_t a, size_t b, void* db, void* ds, hipStream_t cs, hipEvent_t sc_ready,
-                         hipEvent_t b_ready) -> int {
-      // gather piece [a, b) on the host pool (scalars, then bases: the scalar DMA overlaps the
-      // base gather, and this piece's DMA the next piece's gather)
+    // gather piece [a, b) on the host pool (scalars, then bases: the scalar DMA and the piece's
+    // sort overlap the base gather, and this piece's DMA the next piece's gather)
+    feed.stage_scalars = [&, lo](size_t a, size_t b, void* ds, hipStream_t cs, hipEvent_t ready) -> int {
       host_parallel_for(b - a, 8192, [&](size_t x, size_t y) {
         for (size_t i = a + x; i < a + y; i++) {
           if (i + kGatherAhead < a + y) __builtin_prefetch(pairs[lo + i + kGatherAhead].scalar);
@@ -267,7 +269,10 @@ int sv_bn254_g1_msm_refs(const sv_msm_ref* pairs, size_t n, int form, int num_gp
         }
       });
       SV_HIP(hipMemcpyAsync(ds, hs + a, (b - a) * sizeof(sv_fe), hipMemcpyHostToDevice, cs));
-      SV_HIP(hipEventRecord(sc_ready, cs));
+      SV_HIP(hipEventRecord(ready, cs));
+      return SV_OK;
+    };
+    feed.stage_bases = [&, lo](size_t a, size_t b, void* db, hipStream_t cs, hipEvent_t ready) -> int {
       host_parallel_for(b - a, 8192, [&](size_t x, size_t y) {
         for (size_t i = a + x; i < a + y; i++) {
           if (i + kGatherAhead < a + y) {
@@ -285,7 +290,7 @@ int sv_bn254_g1_msm_refs(const sv_msm_ref* pairs, size_t n, int form, int num_gp
         }
       });
       SV_HIP(hipMemcpyAsync(db, hb + a, (b - a) * sizeof(sv_g1_affine), hipMemcpyHostToDevice, cs));
-      SV_HIP(hipEventRecord(b_ready, cs));
+      SV_HIP(hipEventRecord(ready, cs));
       return SV_OK;
     };
     int r = msm_run_fed(m, form, dev, feed, &part[k]);

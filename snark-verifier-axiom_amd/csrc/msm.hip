@@ -33,6 +33,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <vector>
 
 #include "curve.hpp"
@@ -1030,7 +1031,8 @@ static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, 
                      int mont_in, int device, hipStream_t st, G1Xyzz* bsum, const uint4* phix, uint32_t nsplit,
                      hipEvent_t ev_sorted, hipEvent_t ev_sort_mid, hipEvent_t ev_acc_done, hipEvent_t ev_fix_mid,
                      hipEvent_t bases_ready, const G1Aff* conv_src, hipStream_t side = nullptr,
-                     hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr) {
+                     hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr,
+                     const std::function<int()>& stage_bases = nullptr) {
   const int LOGB = p.c - 1;
   const int nb = p.glv ? 128 : 255;
   const uint32_t CB = (uint32_t)coarse_bits(p.c, nb), FB = (uint32_t)LOGB - CB, NBIN = 1u << CB;
@@ -1075,6 +1077,7 @@ static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, 
     SV_HIP(hipStreamWaitEvent(st, ev_join, 0));
   }
   SV_HIP(hipGetLastError());
+  if (stage_bases) SV_TRY(stage_bases());  // host-fed: the bases' transfer, after the sort is queued
   if (bases_ready) SV_HIP(hipStreamWaitEvent(st, bases_ready, 0));
   if (conv_src)  // host-fed canonical bases: converted once they have landed, after the sort
     hipLaunchKernelGGL(k_to_mont_bases, dim3(cdiv(npts, kBlock)), dim3(kBlock), 0, st, conv_src,
@@ -1115,13 +1118,16 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   Workspace* ws = lease.get();
   hipStream_t st = ws->stream;
   // host-fed inputs arrive in pieces: piece k's sort + accumulate run while piece k + 1 is in flight
+  MsmPlan p = msm_plan(n);
   int pieces = 1;
   if (feed) {
-    pieces = feed->pieces < 1 ? 1 : feed->pieces;
+    // default: 2 pieces with GLV, 4 without (tools/host_api_bench.py at 2^20: GLV 3.17 ms with 2,
+    // 3.34 with 4 -- each piece's accumulate over a quarter of the points runs at ~70 % of the whole
+    // one's rate; no GLV 3.34 / 3.25)
+    pieces = feed->pieces > 0 ? feed->pieces : (p.glv ? 2 : 4);
     if (n < (size_t)pieces * 4096) pieces = 1;
     if (pieces > 8) pieces = 8;
   }
-  MsmPlan p = msm_plan(n);
   const size_t max_piece = (n + pieces - 1) / pieces;
   const uint32_t ep = p.glv ? 2 * p.W : p.W;  // entries per real point
   const uint64_t entries = (uint64_t)max_piece * ep;  // per piece
@@ -1239,8 +1245,9 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
       hipEvent_t sc_ready = ws->ev[8 + 2 * k], b_ready = ws->ev[9 + 2 * k];
       G1Aff* db = const_cast<G1Aff*>(reinterpret_cast<const G1Aff*>(d_bases)) + lo;
       Fr* dsc = const_cast<Fr*>(scalars) + lo;
-      SV_TRY(feed->stage(lo, hi, db, dsc, cs, sc_ready, b_ready));
+      SV_TRY(feed->stage_scalars(lo, hi, dsc, cs, sc_ready));
       SV_HIP(hipStreamWaitEvent(st, sc_ready, 0));
+      const std::function<int()> stage_b = [&]() { return feed->stage_bases(lo, hi, db, cs, b_ready); };
       if (k > 0) SV_HIP(hipMemsetAsync(w.err + 1, 0, 8, st));  // fixup queue counters
       const G1Aff* pb = conv ? bases_m + lo : db;
       G1Xyzz* dst = k == 0 ? bsum : bsum_k;
@@ -1248,7 +1255,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
       uint4* phix_k = p.glv ? phix + (size_t)(p.phi64 ? 4 : 2) * lo : nullptr;
       SV_TRY(msm_front(p, w, pb, dsc, m, mont_in, device, st, dst, phix_k, p.glv ? (uint32_t)m : ~0u,
                        k == 0 ? ev[2] : nullptr, nullptr, k == pieces - 1 ? ev[3] : nullptr, nullptr, b_ready,
-                       conv ? db : nullptr));
+                       conv ? db : nullptr, nullptr, nullptr, nullptr, stage_b));
       if (pieces > 1) {
         if (k == 0) {
           SV_HIP(hipMemcpyAsync(gst0, w.gst, ((size_t)p.nbt + 1) * 4, hipMemcpyDeviceToDevice, st));

@@ -34,14 +34,15 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
                    hipStream_t stream, host::Xyzz* out);
 
 // Host-fed MSM (the host-buffer entry points): the caller's inputs reach HBM in `pieces` pieces on
-// the workspace's copy stream.  stage(lo, hi, d_bases, d_scalars, copy_stream, scalars_ready,
-// bases_ready) issues the transfers of points [lo, hi) into the given device pointers and records
-// the two events (scalars first: the piece's sort starts as soon as they land).
+// the workspace's copy stream.  stage_scalars(lo, hi, d_scalars, copy_stream, ready) and
+// stage_bases(lo, hi, d_bases, copy_stream, ready) issue the transfers of points [lo, hi) into the
+// given device pointers and record `ready` after them.  They are called in that order per piece,
+// with the piece's sort enqueued in between: pageable transfers block the calling thread, so the
+// sort then runs while the bases are still in flight.
 struct MsmFeed {
   int pieces = 4;
-  std::function<int(size_t lo, size_t hi, void* d_bases, void* d_scalars, hipStream_t copy_stream,
-                    hipEvent_t scalars_ready, hipEvent_t bases_ready)>
-      stage;
+  std::function<int(size_t lo, size_t hi, void* d_scalars, hipStream_t copy_stream, hipEvent_t ready)> stage_scalars;
+  std::function<int(size_t lo, size_t hi, void* d_bases, hipStream_t copy_stream, hipEvent_t ready)> stage_bases;
 };
 int msm_run_fed(size_t n, int form, int device, const MsmFeed& feed, host::Xyzz* out);
 

@@ -17,7 +17,7 @@
 //                     load balance whatever the digit distribution), complete buckets written
 //                     directly, bucket pieces that cross a thread boundary to pfirst/plast
 //                     (two-piece buckets inside a block are joined at the end through LDS)
-//   k_fixup_multi     the other crossing buckets, queued by k_accumulate (k_fixup_heavy: block-level
+//   k_fixup           the other crossing buckets, queued by k_accumulate (heavy ones: block-level
 //                     tree for buckets spanning more than 9 threads)
 //   k_wsum            bucket reduction, step 1: F_w = sum_b (b+1) S_b = sum_j acc_j + L sum_j j T_j
 //                     with running sums over segments of L = 8 buckets (acc_j, T_j per segment)
@@ -592,9 +592,9 @@ __global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__
 // for random scalars -- is joined here: the head goes to LDS, and after the barrier the owner adds
 // it to the piece still in its registers (one extra addition per owner at the accumulate's full
 // occupancy, no global round trip).  Every other crossing bucket keeps the global pieces
-// (pfirst = a thread's first segment, plast = its last) and is queued for k_fixup_multi.  Empty
+// (pfirst = a thread's first segment, plast = its last) and is queued for k_fixup.  Empty
 // buckets are never written: k_wsum reads gst.
-static constexpr uint32_t kFixSerial = 8;  // crossing buckets of more pieces go to k_fixup_heavy
+static constexpr uint32_t kFixSerial = 8;  // crossing buckets of more pieces: k_fixup's heavy blocks
 __device__ __forceinline__ bool join_in_block(uint32_t gs, uint32_t ge, uint32_t K) {
   const uint32_t t0 = gs / K, t1 = (ge - 1) / K;
   return t1 == t0 + 1 && t0 / kBlock == t1 / kBlock;
@@ -678,7 +678,7 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
       owner = true;
     } else {
       store_xyzz(first ? pfirst : plast, t, acc);
-      multi[atomicAdd(nmulti, 1u)] = g;  // joined by k_wsum (device path) or k_fixup_multi (host-fed)
+      multi[atomicAdd(nmulti, 1u)] = g;  // joined by k_fixup
       if ((ge - 1) / K - gs / K > kFixSerial) heavy[atomicAdd(nheavy, 1u)] = g;
     }
   }
@@ -688,42 +688,42 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
 
 // Queued crossing buckets (see k_accumulate): pieces pfirst/plast joined serially when the bucket
 // spans at most kFixSerial + 1 threads; longer ones (skewed digits: all-equal scalars, a short top
-// window) are queued by k_accumulate for k_fixup_heavy instead of being walked serially.
+// window) are queued by k_accumulate for k_fixup's heavy blocks instead of being walked serially.
 __device__ __forceinline__ G1Xyzz fixup_head(const G1Xyzz* __restrict__ pfirst, const G1Xyzz* __restrict__ plast,
                                              uint32_t s, uint32_t t0, uint32_t K) {
   return (s == t0 * K) ? load_xyzz(pfirst, t0) : load_xyzz(plast, t0);
 }
 
-// grid-stride over the queue
-__global__ void __launch_bounds__(kBlock) k_fixup_multi(const uint32_t* __restrict__ gst, uint32_t K,
-                                                        const G1Xyzz* __restrict__ pfirst,
-                                                        const G1Xyzz* __restrict__ plast,
-                                                        const uint32_t* __restrict__ multi,
-                                                        const uint32_t* __restrict__ nmulti, G1Xyzz* __restrict__ bsum,
-                                                        uint32_t* __restrict__ heavy, uint32_t* __restrict__ nheavy) {
-  const uint32_t nm = *nmulti;
-  for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < nm; h += gridDim.x * blockDim.x) {
-    const uint32_t g = multi[h];
-    const uint32_t s = gst[g], e = gst[g + 1];
-    const uint32_t t0 = s / K, t1 = (e - 1) / K;
-    if (t1 - t0 > kFixSerial) continue;  // queued for k_fixup_heavy by k_accumulate
-    G1Xyzz acc = fixup_head(pfirst, plast, s, t0, K);
-    for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, load_xyzz(pfirst, t));
-    store_xyzz(bsum, g, acc);
-  }
-}
-
-// Heavy buckets: one block per queued bucket (grid-stride over the queue), strided partial sums of
-// the per-thread pieces + LDS tree.
-__global__ void __launch_bounds__(kBlock) k_fixup_heavy(const uint32_t* __restrict__ gst, uint32_t K,
-                                                        const G1Xyzz* __restrict__ pfirst,
-                                                        const G1Xyzz* __restrict__ plast,
-                                                        const uint32_t* __restrict__ heavy,
-                                                        const uint32_t* __restrict__ nheavy,
-                                                        G1Xyzz* __restrict__ bsum) {
+// One launch for both queues: blocks [0, gm) walk the multi queue (grid-stride, one bucket per
+// thread, a serial chain of at most kFixSerial 2p-domain additions), blocks [gm, gridDim) take the
+// heavy queue (one bucket per block: strided partial sums of the per-thread pieces + LDS tree).
+// The two queues hold disjoint buckets (k_accumulate puts a bucket of more than kFixSerial + 1
+// pieces in both; the multi walk skips it).
+__global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ gst, uint32_t K,
+                                                  const G1Xyzz* __restrict__ pfirst,
+                                                  const G1Xyzz* __restrict__ plast,
+                                                  const uint32_t* __restrict__ multi,
+                                                  const uint32_t* __restrict__ nmulti,
+                                                  const uint32_t* __restrict__ heavy,
+                                                  const uint32_t* __restrict__ nheavy, uint32_t gm,
+                                                  G1Xyzz* __restrict__ bsum) {
   __shared__ G1Xyzz sh[kBlock];
-  const uint32_t nh = *nheavy, tid = threadIdx.x;
-  for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {
+  const uint32_t tid = threadIdx.x;
+  if (blockIdx.x < gm) {  // block-uniform
+    const uint32_t nm = *nmulti;
+    for (uint32_t h = blockIdx.x * blockDim.x + tid; h < nm; h += gm * blockDim.x) {
+      const uint32_t g = multi[h];
+      const uint32_t s = gst[g], e = gst[g + 1];
+      const uint32_t t0 = s / K, t1 = (e - 1) / K;
+      if (t1 - t0 > kFixSerial) continue;  // a heavy bucket: the other blocks' part
+      G1Xyzz acc = fixup_head(pfirst, plast, s, t0, K);
+      for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add_2p(acc, load_xyzz(pfirst, t));
+      store_xyzz(bsum, g, xyzz_canon2p(acc));
+    }
+    return;
+  }
+  const uint32_t nh = *nheavy, gh = gridDim.x - gm;
+  for (uint32_t h = blockIdx.x - gm; h < nh; h += gh) {
     const uint32_t g = heavy[h];
     const uint32_t s = gst[g], e = gst[g + 1];
     const uint32_t t0 = s / K, t1 = (e - 1) / K;
@@ -760,7 +760,7 @@ __global__ void __launch_bounds__(kBlock) k_merge_buckets(G1Xyzz* __restrict__ a
 
 // Bucket i of one window (x, gs: that window's bucket sums and starts): false when empty.
 // gs == null: every bucket was written (host-fed merge).  (Joining the crossing buckets here
-// instead of in k_fixup_multi was measured 155 -> 440 us for k_wsum at 2^20: ~7 % of buckets cross,
+// instead of in k_fixup was measured 155 -> 440 us for k_wsum at 2^20: ~7 % of buckets cross,
 // so nearly every wave's iteration diverges into the join loop.)
 __device__ __forceinline__ bool bucket_at(const G1Xyzz* __restrict__ x, const uint32_t* __restrict__ gs, uint32_t i,
                                           G1Xyzz& out) {
@@ -1090,10 +1090,9 @@ static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, 
                      p.nbt, p.K, T, bsum, w.pfirst, w.plast, w.multi, w.nmulti, w.heavy, w.nheavy, phix, nsplit, p.phi64);
   SV_HIP(hipGetLastError());
   if (ev_acc_done) SV_HIP(hipEventRecord(ev_acc_done, st));
-  hipLaunchKernelGGL(k_fixup_multi, dim3(std::min<uint32_t>(cdiv(p.nbt, kBlock), 1024)), dim3(kBlock), 0, st,
-                     w.gst, p.K, w.pfirst, w.plast, w.multi, w.nmulti, bsum, w.heavy, w.nheavy);
-  hipLaunchKernelGGL(k_fixup_heavy, dim3(256), dim3(kBlock), 0, st, w.gst, p.K, w.pfirst, w.plast, w.heavy,
-                     w.nheavy, bsum);
+  const uint32_t gm = std::min<uint32_t>(cdiv(p.nbt, kBlock), 1024);
+  hipLaunchKernelGGL(k_fixup, dim3(gm + 256), dim3(kBlock), 0, st, w.gst, p.K, w.pfirst, w.plast, w.multi, w.nmulti,
+                     w.heavy, w.nheavy, gm, bsum);
   SV_HIP(hipGetLastError());
   if (ev_fix_mid) SV_HIP(hipEventRecord(ev_fix_mid, st));
   return SV_OK;

@@ -1,4 +1,4 @@
-# Round-2 final evidence in one GPU session: gpu tests, smoke, full bench (CPU baseline + config-4 parity),
+# Round-2 evidence in one GPU session: gpu tests, smoke, full bench (CPU baseline + config-4 parity),
 # rocprof kernel-trace stats (headline + extras), separate FETCH_SIZE / WRITE_SIZE passes, the
 # FETCH_SIZE calibration of the gather pattern, and the N=2 gloo rehearsal.  Stops at the first failure.
 cd "$GRAFT_REPO_ROOT"

@@ -2,11 +2,7 @@
 
 #include <cstdarg>
 #include <cstdio>
-#include <atomic>
-#include <chrono>
-#include <condition_variable>
 #include <cstdlib>
-#include <thread>
 
 namespace sv {
 
@@ -101,89 +97,6 @@ int Workspace::ensure_copy_stream() {
   SV_HIP(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
   return SV_OK;
 }
-
-namespace {
-// Fixed pool of host workers; one job at a time (concurrent callers queue on job_mu).  A job is
-// split into one slice per thread, claimed dynamically; workers spin for a while after each job
-// before sleeping, because the host-fed MSM issues its gather jobs in bursts (a futex wake-up
-// costs about as much as a whole slice, so sleeping workers left the caller doing every slice).
-class HostPool {
- public:
-  HostPool() {
-    int hw = (int)std::thread::hardware_concurrency();
-    nthreads_ = hw > 16 ? 16 : (hw > 0 ? hw : 1);
-    if (const char* e = getenv("SVGPU_HOST_THREADS")) nthreads_ = atoi(e) > 0 ? atoi(e) : 1;
-    for (int i = 1; i < nthreads_; i++) workers_.emplace_back([this] { loop(); });
-    for (auto& w : workers_) w.detach();  // the pool lives for the process
-  }
-  int threads() const { return nthreads_; }
-  void run(size_t n, size_t grain, const std::function<void(size_t, size_t)>& fn) {
-    if (n == 0) return;
-    size_t parts = (n + grain - 1) / (grain ? grain : 1);
-    if (parts > (size_t)nthreads_) parts = (size_t)nthreads_;
-    if (parts <= 1) {
-      fn(0, n);
-      return;
-    }
-    std::lock_guard<std::mutex> job(job_mu_);
-    fn_ = &fn;
-    n_ = n;
-    parts_ = parts;
-    next_.store(0, std::memory_order_relaxed);
-    done_.store(0, std::memory_order_relaxed);
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      gen_.fetch_add(1, std::memory_order_release);
-    }
-    cv_.notify_all();
-    work();
-    while (done_.load(std::memory_order_acquire) != parts_) std::this_thread::yield();
-  }
-
- private:
-  void work() {
-    for (;;) {
-      const size_t k = next_.fetch_add(1, std::memory_order_acq_rel);
-      if (k >= parts_) return;
-      (*fn_)(n_ * k / parts_, n_ * (k + 1) / parts_);
-      done_.fetch_add(1, std::memory_order_acq_rel);
-    }
-  }
-  void loop() {
-    uint64_t seen = 0;
-    for (;;) {
-      // spin ~1 ms for the next job of a burst, then sleep
-      auto t0 = std::chrono::steady_clock::now();
-      while (gen_.load(std::memory_order_acquire) == seen &&
-             std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(1))
-        std::this_thread::yield();
-      if (gen_.load(std::memory_order_acquire) == seen) {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
-      }
-      seen = gen_.load(std::memory_order_acquire);
-      work();
-    }
-  }
-  int nthreads_ = 1;
-  std::vector<std::thread> workers_;
-  std::mutex job_mu_, mu_;
-  std::condition_variable cv_;
-  const std::function<void(size_t, size_t)>* fn_ = nullptr;
-  size_t n_ = 0, parts_ = 0;
-  std::atomic<size_t> next_{0}, done_{0};
-  std::atomic<uint64_t> gen_{0};
-};
-HostPool& host_pool() {
-  static HostPool* p = new HostPool();  // leaked: detached workers outlive static destruction
-  return *p;
-}
-}  // namespace
-
-void host_parallel_for(size_t n, size_t grain, const std::function<void(size_t, size_t)>& fn) {
-  host_pool().run(n, grain, fn);
-}
-int host_threads() { return host_pool().threads(); }
 
 int runtime_init(int num_devices) {
   std::lock_guard<std::mutex> lk(g_init_mu);

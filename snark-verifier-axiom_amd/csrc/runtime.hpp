@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/svgpu.h"
+#include "hostpool.hpp"
 
 namespace sv {
 
@@ -53,11 +54,6 @@ struct Workspace {
   int reserve_stage(size_t bytes);   // grow-only pinned gather staging
   int ensure_copy_stream();
 };
-
-// Host worker pool shared by every call (SVGPU_HOST_THREADS, default min(16, cores)): fn(lo, hi)
-// over contiguous slices of [0, n) of at least `grain` items, run on the pool and the caller.
-void host_parallel_for(size_t n, size_t grain, const std::function<void(size_t, size_t)>& fn);
-int host_threads();
 
 // RAII lease of a per-device workspace; stream override optional.
 class WsLease {

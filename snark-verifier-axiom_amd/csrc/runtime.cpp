@@ -67,7 +67,7 @@ int Workspace::reserve_in(size_t bytes) {
   if (bytes <= in_cap) return SV_OK;
   SV_HIP(hipSetDevice(device));
   if (inbuf) {
-    SV_HIP(hipStreamSynchronize(stream));
+    SV_TRY(quiesce());  // a DMA of an earlier (failed) call may still target inbuf
     SV_HIP(hipFree(inbuf));
     inbuf = nullptr;
     in_cap = 0;
@@ -83,11 +83,21 @@ int Workspace::reserve_in(size_t bytes) {
 
 int Workspace::reserve_stage(size_t bytes) {
   if (bytes <= stage_cap) return SV_OK;
-  if (stage) SV_HIP(hipHostFree(stage));
+  if (stage) {
+    SV_TRY(quiesce());  // the copy stream may still be reading the staging
+    SV_HIP(hipHostFree(stage));
+  }
   stage = nullptr;
   stage_cap = 0;
   SV_HIP(hipHostMalloc(&stage, bytes, hipHostMallocDefault));
   stage_cap = bytes;
+  return SV_OK;
+}
+
+int Workspace::quiesce() {
+  SV_HIP(hipSetDevice(device));
+  if (stream) SV_HIP(hipStreamSynchronize(stream));
+  if (copy_stream) SV_HIP(hipStreamSynchronize(copy_stream));
   return SV_OK;
 }
 
@@ -107,10 +117,42 @@ int runtime_init(int num_devices) {
     set_error("no usable GPU (hipGetDeviceCount: %s, count=%d)", hipGetErrorString(e), count);
     return SV_ERR_DEVICE;
   }
-  if (num_devices > 0 && num_devices < count) count = num_devices;
-  for (int d = 0; d < count; d++) {
-    auto* p = new DevicePool();
-    p->device = d;
+  // SVGPU_DEVICE_MAP=a,b,...: logical device i runs on HIP device map[i] (repeats allowed).  With
+  // "0,0,0,0,0,0,0,0" the multi-device host paths (one host thread per logical device, each with
+  // its own workspace and streams, partials folded on the host) run 8-wide on one physical GPU.
+  std::vector<int> map;
+  if (const char* e = getenv("SVGPU_DEVICE_MAP")) {
+    for (const char* q = e; *q;) {
+      char* end = nullptr;
+      const long d = strtol(q, &end, 10);
+      if (end == q || d < 0 || d >= count) {
+        set_error("SVGPU_DEVICE_MAP=\"%s\": bad entry (HIP devices 0..%d)", e, count - 1);
+        return SV_ERR_ARG;
+      }
+      map.push_back((int)d);
+      q = *end == ',' ? end + 1 : end;
+      if (*end && *end != ',') {
+        set_error("SVGPU_DEVICE_MAP=\"%s\": expected comma-separated device ordinals", e);
+        return SV_ERR_ARG;
+      }
+    }
+  } else {
+    for (int d = 0; d < count; d++) map.push_back(d);
+  }
+  if (map.empty()) {
+    set_error("SVGPU_DEVICE_MAP is empty");
+    return SV_ERR_ARG;
+  }
+  if (num_devices > 0 && (size_t)num_devices < map.size()) map.resize(num_devices);
+  for (int d : map) {
+    // logical devices on the same HIP device share its workspace pool (each call leases its own)
+    DevicePool* p = nullptr;
+    for (auto* q : g_pools)
+      if (q->device == d) p = q;
+    if (!p) {
+      p = new DevicePool();
+      p->device = d;
+    }
     g_pools.push_back(p);
   }
   return SV_OK;

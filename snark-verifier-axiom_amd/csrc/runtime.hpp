@@ -53,6 +53,7 @@ struct Workspace {
   int reserve_in(size_t bytes);      // grow-only device input buffer
   int reserve_stage(size_t bytes);   // grow-only pinned gather staging
   int ensure_copy_stream();
+  int quiesce();  // wait for the compute and copy streams (before freeing or reusing staging)
 };
 
 // RAII lease of a per-device workspace; stream override optional.

@@ -189,10 +189,13 @@ pub fn available() -> bool {
     })
 }
 
-/// Reinterpret a generic curve's slices as BN254 ones.  Call only after
-/// `TypeId::of::<C>() == TypeId::of::<G1Affine>()` (the call sites in snark-verifier check it).
-pub fn cast_slices<'a, C: 'static>(scalars: &'a [impl Sized], bases: &'a [C]) -> (&'a [Fr], &'a [G1Affine]) {
-    assert_eq!(std::any::TypeId::of::<C>(), std::any::TypeId::of::<G1Affine>());
+/// Reinterpret a generic curve's slices as BN254 ones.  Both element types are checked at run
+/// time (scalars must be `Fr`, bases `G1Affine`), so the cast is a no-op view of the same types
+/// and the function is sound for any caller; it panics on any other pair of types.
+pub fn cast_slices<'a, S: 'static, C: 'static>(scalars: &'a [S], bases: &'a [C]) -> (&'a [Fr], &'a [G1Affine]) {
+    assert_eq!(std::any::TypeId::of::<S>(), std::any::TypeId::of::<Fr>(), "scalars are not bn256::Fr");
+    assert_eq!(std::any::TypeId::of::<C>(), std::any::TypeId::of::<G1Affine>(), "bases are not bn256::G1Affine");
+    // SAFETY: S == Fr and C == G1Affine (checked above): same type, same length, same lifetime
     unsafe {
         (std::slice::from_raw_parts(scalars.as_ptr() as *const Fr, scalars.len()),
          std::slice::from_raw_parts(bases.as_ptr() as *const G1Affine, bases.len()))
@@ -231,8 +234,9 @@ pub fn msm(pairs: &[(&Fr, &G1Affine)]) -> Option<G1Affine> {
 pub fn msm_slices(scalars: &[Fr], bases: &[G1Affine]) -> Option<G1Affine> {
     assert_eq!(scalars.len(), bases.len());
     if bases.is_empty() {
-        // msm.rs:238-316 returns the identity for an empty MSM
-        return Some(<G1Affine as halo2curves::group::prime::PrimeCurveAffine>::identity());
+        // the reference panics on an empty MSM: multi_scalar_multiplication_serial indexes
+        // scalars[0] (msm.rs:244), reached with or without `parallel` (msm.rs:295-298, :313-314)
+        panic!("index out of bounds: the len is 0 but the index is 0");
     }
     let mut out = SvG1Affine::default();
     let rc = unsafe {

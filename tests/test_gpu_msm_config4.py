@@ -71,3 +71,32 @@ def test_msm_2_24_eight_shards_fold_to_whole(inputs_2_24, oracle_2_24):
     assert svgpu.fold_partials(parts) == oracle_2_24
     # the fold is order-independent as a group sum, but the rank-order fold is what every rank runs
     assert svgpu.fold_partials(parts[::-1]) == oracle_2_24
+
+
+@pytest.mark.timeout(600)
+def test_logical_devices_host_paths_8_wide(oracle_2_24):
+    """The in-process multi-device path (what the Rust shim gets with num_gpus = 0 on an 8-GPU node:
+    api.cpp for_each_device, one host thread + workspace lease + copy stream per device, host fold /
+    first_fail combine) run 8-wide on this box's one GPU through SVGPU_DEVICE_MAP=0,...,0:
+    sv_bn254_g1_msm(num_gpus=8) and sv_bn254_g1_msm_refs(num_gpus=8) at 2^24 equal the oracle, the
+    uneven 3-way split too, and sv_bn254_kzg_decide(num_gpus=8) over 256 accumulators with failures
+    at 37 and 200 reports 37 (decider.rs:70-80 try_collect: the first Err)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = dict(os.environ, SVGPU_DEVICE_MAP=",".join(["0"] * 8))
+    child = os.path.join(ROOT, "tests", "logical_devices_child.py")
+    r = subprocess.run([sys.executable, "-u", child, str(LOG_N), "8"], env=env, capture_output=True, text=True,
+                       timeout=540)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")][-1]
+    res = json.loads(line[len("RESULT "):])
+    exp = [hex(oracle_2_24[0]), hex(oracle_2_24[1])]
+    assert res["device_count"] == 8
+    assert res["msm"] == exp
+    assert res["msm_3"] == exp
+    assert res["msm_refs"] == exp
+    assert res["decide_first_fail"] == 37
+    assert res["decide_all_pass"] == -1

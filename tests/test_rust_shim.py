@@ -50,3 +50,34 @@ def test_rust_structs_match_header_fields():
     names = re.findall(r"([a-z_]+)[,;]", fields)
     rnames = re.findall(r"pub ([a-z_]+): (?:f32|u32|u64)", rs[rs.index("pub struct SvMsmStats"):])
     assert names == rnames
+
+
+def _fn_body(rs, name):
+    start = rs.index("pub fn " + name)
+    body = rs[start:]
+    return body[:body.index("\n}\n")]
+
+
+def test_cast_slices_checks_both_element_types():
+    """cast_slices is a safe fn, so it must be sound for ANY caller: it asserts the scalar type
+    (Fr) as well as the curve type (G1Affine) before reinterpreting the slices."""
+    rs = open(os.path.join(ROOT, "snark-verifier-gpu", "src", "lib.rs")).read()
+    sig = re.search(r"pub (unsafe )?fn cast_slices<'a, S: 'static, C: 'static>\(scalars: &'a \[S\], bases: &'a \[C\]\)", rs)
+    assert sig, "cast_slices must be generic over the scalar type too"
+    body = _fn_body(rs, "cast_slices")
+    assert "TypeId::of::<S>(), std::any::TypeId::of::<Fr>()" in body
+    assert "TypeId::of::<C>(), std::any::TypeId::of::<G1Affine>()" in body
+    assert body.index("TypeId::of::<S>") < body.index("unsafe {")
+
+
+def test_msm_slices_panics_on_empty_like_the_reference():
+    """msm.rs:244 indexes scalars[0], so the reference panics on an empty MSM; the wrapper must not
+    return the identity instead."""
+    rs = open(os.path.join(ROOT, "snark-verifier-gpu", "src", "lib.rs")).read()
+    body = _fn_body(rs, "msm_slices")
+    empty = body[body.index("if bases.is_empty()"):]
+    empty = empty[:empty.index("}")]
+    assert "panic!" in empty and "identity" not in empty
+    ref = open("/root/reference/snark-verifier/src/util/msm.rs").read() if os.path.exists("/root/reference") else None
+    if ref is not None:
+        assert "let num_bytes = scalars[0].as_ref().len();" in ref

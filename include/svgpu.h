@@ -66,9 +66,12 @@ const char* sv_version(void) SV_NOEXCEPT;
 /* ---- a1/a3: multi-scalar multiplication ---------------------------------------------
  * out = sum_i scalars[i] * bases[i] as an affine point (identity -> (0,0)).
  * Host buffers.  num_gpus <= 0 means every initialised device (point-sharded, partials
- * folded in device order).  Scalars must be reduced (< r) in the given form.  The inputs
- * reach HBM in pieces (SVGPU_H2D_PIECES, default 4) on a copy stream, each piece's sort and
- * bucket accumulation overlapping the next piece's transfer; device buffers are pooled.   */
+ * folded in device order).  Scalars must be reduced (< r) and base coordinates reduced
+ * (< p) in the given form, else SV_ERR_ARG.  The inputs reach HBM in pieces on a copy
+ * stream (default: 6 pieces weighted 2,2,3,3,3,3 from 2^18 points, 2 from 2^15, else 1;
+ * SVGPU_H2D_PIECES = N equal pieces, SVGPU_H2D_SPLIT = comma-separated weights); each
+ * piece is sorted on a second stream once its scalars land and accumulated into the one
+ * bucket set once its bases land, while later pieces are in flight; buffers are pooled.   */
 int sv_bn254_g1_msm(const sv_g1_affine* bases, const sv_fe* scalars, size_t n, int form,
                     int num_gpus, sv_g1_affine* out) SV_NOEXCEPT;
 

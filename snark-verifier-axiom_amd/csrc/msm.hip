@@ -209,9 +209,10 @@ struct Digits {
 };
 
 // GLV: phi(P_i) = (beta x_i, y_i); only beta x_i is stored (phix[i], 32 B, written by k_bin_hist),
-// the accumulate reads y_i from the bases (identity (0, 0) maps to itself).
+// the accumulate reads y_i from the bases (identity (0, 0) maps to itself).  With err set the point's
+// coordinates are checked to be reduced (Montgomery input is used as is by the 2p-domain adds).
 __device__ __forceinline__ void glv_phix(const G1Aff* __restrict__ bases, uint32_t i, uint4* __restrict__ phix,
-                                         int phi64) {
+                                         int phi64, uint32_t* __restrict__ err) {
   const uint4* b = reinterpret_cast<const uint4*>(bases + i);
   Fq x, beta;
   const uint4 x0 = b[0], x1 = b[1];
@@ -223,16 +224,34 @@ __device__ __forceinline__ void glv_phix(const G1Aff* __restrict__ bases, uint32
   uint4* o = phix + (phi64 ? 4 : 2) * i;
   o[0] = make_uint4(bx.v[0], bx.v[1], bx.v[2], bx.v[3]);
   o[1] = make_uint4(bx.v[4], bx.v[5], bx.v[6], bx.v[7]);
-  if (phi64) {
-    o[2] = b[2];
-    o[3] = b[3];
+  if (phi64 || err) {
+    const uint4 y0 = b[2], y1 = b[3];
+    if (phi64) {
+      o[2] = y0;
+      o[3] = y1;
+    }
+    if (err) {
+      Fq y;
+      y.v[0] = y0.x; y.v[1] = y0.y; y.v[2] = y0.z; y.v[3] = y0.w;
+      y.v[4] = y1.x; y.v[5] = y1.y; y.v[6] = y1.z; y.v[7] = y1.w;
+      if (!x.is_reduced() || !y.is_reduced()) atomicOr(err, 1u);
+    }
   }
 }
 
 // Host-fed pieces: the piece's table once its bases have landed (its sort ran on the scalars alone)
-__global__ void k_glv_phix(const G1Aff* __restrict__ bases, uint32_t n, uint4* __restrict__ phix, int phi64) {
+__global__ void k_glv_phix(const G1Aff* __restrict__ bases, uint32_t n, uint4* __restrict__ phix, int phi64,
+                           uint32_t* __restrict__ err) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) glv_phix(bases, i, phix, phi64);
+  if (i < n) glv_phix(bases, i, phix, phi64, err);
+}
+
+// Montgomery-form bases that no other pass reads before the accumulate (no GLV table, host-fed)
+__global__ void k_check_bases(const G1Aff* __restrict__ bases, uint32_t n, uint32_t* __restrict__ err) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const G1Aff a = load_aff(bases, i);
+  if (!a.x.is_reduced() || !a.y.is_reduced()) atomicOr(err, 1u);
 }
 
 // ---- two-level counting sort of the n * W (point, digit) entries by bucket ------------------
@@ -305,7 +324,7 @@ template <int C, bool GLV>
 __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scalars, uint32_t n, int mont_in,
                                                      uint32_t nblk, uint32_t* __restrict__ bcnt,
                                                      uint32_t* __restrict__ err, const G1Aff* __restrict__ bases,
-                                                     uint4* __restrict__ phix, int phi64) {
+                                                     uint4* __restrict__ phix, int phi64, int check_bases) {
   using D = Digits<C, GLV>;
   constexpr int W = D::W, LOGB = C - 1;
   constexpr int CB = coarse_bits(C, D::NB), FB = LOGB - CB, NBIN = 1 << CB;
@@ -315,8 +334,14 @@ __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scal
   constexpr uint32_t CH = sort_chunk(D::EP);
   const uint32_t lo = blockIdx.x * CH, hi = min(n, lo + CH);
   for (uint32_t i = lo + threadIdx.x; i < hi; i += kBlock) {
+    // Montgomery bases are checked here (canonical ones by k_to_mont_bases)
     if constexpr (GLV) {
-      if (phix) glv_phix(bases, i, phix, phi64);  // (null: bases not landed yet, k_glv_phix later)
+      if (phix) glv_phix(bases, i, phix, phi64, check_bases ? err : nullptr);  // (null: bases not landed yet, k_glv_phix later)
+    } else {
+      if (check_bases) {
+        const G1Aff a = load_aff(bases, i);
+        if (!a.x.is_reduced() || !a.y.is_reduced()) atomicOr(err, 1u);
+      }
     }
     D d;
     d.load(scalars, i, mont_in, err);
@@ -599,6 +624,14 @@ __device__ __forceinline__ bool join_in_block(uint32_t gs, uint32_t ge, uint32_t
   const uint32_t t0 = gs / K, t1 = (ge - 1) / K;
   return t1 == t0 + 1 && t0 / kBlock == t1 / kBlock;
 }
+// A complete bucket sum: stored, or (ADD: host-fed pieces after the first, into a bucket set that
+// started as all identity) added to the sum the earlier pieces left there.
+template <bool ADD>
+__device__ __forceinline__ void bucket_put(G1Xyzz* __restrict__ bsum, uint32_t g, const G1Xyzz& v) {
+  if constexpr (ADD) store_xyzz(bsum, g, xyzz_add(v, load_xyzz(bsum, g)));
+  else store_xyzz(bsum, g, v);
+}
+template <bool ADD>
 __global__ void __launch_bounds__(kBlock) k_accumulate(
     const G1Aff* __restrict__ bases, const uint32_t* __restrict__ ent, const uint32_t* __restrict__ gst,
     const uint32_t* __restrict__ tstart, uint32_t nbt, uint32_t K, uint32_t T,
@@ -635,7 +668,7 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
       if (e >= ge) {  // segment [seg_start, ge) of bucket g ends inside this chunk
         acc = xyzz_canon2p(acc);
         if (seg_start == gs) {
-          store_xyzz(bsum, g, acc);
+          bucket_put<ADD>(bsum, g, acc);
         } else {  // head piece of a bucket owned by an earlier thread
           if (join_in_block(gs, ge, K)) shead[threadIdx.x] = acc;
           else store_xyzz(pfirst, t, acc);
@@ -670,7 +703,7 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
     }
     acc = xyzz_canon2p(acc);
     if (seg_start == gs && e_end == ge) {
-      store_xyzz(bsum, g, acc);
+      bucket_put<ADD>(bsum, g, acc);
     } else if (seg_start != gs) {  // first segment, bucket started earlier (it may also go on later)
       if (join_in_block(gs, ge, K)) shead[threadIdx.x] = acc;
       else store_xyzz(pfirst, t, acc);
@@ -683,7 +716,7 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
     }
   }
   __syncthreads();
-  if (owner) store_xyzz(bsum, g, xyzz_add(acc, shead[threadIdx.x + 1]));
+  if (owner) bucket_put<ADD>(bsum, g, xyzz_add(acc, shead[threadIdx.x + 1]));
 }
 
 // Queued crossing buckets (see k_accumulate): pieces pfirst/plast joined serially when the bucket
@@ -699,6 +732,7 @@ __device__ __forceinline__ G1Xyzz fixup_head(const G1Xyzz* __restrict__ pfirst, 
 // heavy queue (one bucket per block: strided partial sums of the per-thread pieces + LDS tree).
 // The two queues hold disjoint buckets (k_accumulate puts a bucket of more than kFixSerial + 1
 // pieces in both; the multi walk skips it).
+template <bool ADD>
 __global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ gst, uint32_t K,
                                                   const G1Xyzz* __restrict__ pfirst,
                                                   const G1Xyzz* __restrict__ plast,
@@ -718,7 +752,7 @@ __global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ g
       if (t1 - t0 > kFixSerial) continue;  // a heavy bucket: the other blocks' part
       G1Xyzz acc = fixup_head(pfirst, plast, s, t0, K);
       for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add_2p(acc, load_xyzz(pfirst, t));
-      store_xyzz(bsum, g, xyzz_canon2p(acc));
+      bucket_put<ADD>(bsum, g, xyzz_canon2p(acc));
     }
     return;
   }
@@ -736,26 +770,10 @@ __global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ g
       __syncthreads();
     }
     if (tid == 0) {
-      store_xyzz(bsum, g, xyzz_add(fixup_head(pfirst, plast, s, t0, K), sh[0]));
+      bucket_put<ADD>(bsum, g, xyzz_add(fixup_head(pfirst, plast, s, t0, K), sh[0]));
     }
     __syncthreads();
   }
-}
-
-// Host-fed pieces: bucket sums of piece k >= 1 (emptiness from its gst) added into piece 0's.  The
-// first merge also reads piece 0's emptiness (gst_acc) and writes every bucket, so afterwards bsum
-// holds all W * B buckets (identity where empty) and k_wsum runs without an emptiness table.
-__global__ void __launch_bounds__(kBlock) k_merge_buckets(G1Xyzz* __restrict__ acc, const uint32_t* __restrict__ gst_acc,
-                                                          const G1Xyzz* __restrict__ x, const uint32_t* __restrict__ gst_x,
-                                                          uint32_t nbt) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nbt) return;
-  const bool ea = gst_acc && gst_acc[b] == gst_acc[b + 1];
-  const bool ex = gst_x[b] == gst_x[b + 1];
-  if (ex && !ea) return;  // nothing to add, acc already written
-  G1Xyzz a = ea ? G1Xyzz::identity() : load_xyzz(acc, b);
-  if (!ex) a = xyzz_add(a, load_xyzz(x, b));
-  store_xyzz(acc, b, a);
 }
 
 // Bucket i of one window (x, gs: that window's bucket sums and starts): false when empty.
@@ -897,6 +915,22 @@ int msm_last_stats(sv_msm_stats* out) {
 
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
+// Sorted entries per accumulate thread for `entries` entries over nbt buckets (SVGPU_ACC_K forces it)
+static uint32_t plan_K(uint64_t entries, uint32_t nbt) {
+  uint64_t K = entries / (1u << 18);
+  if (K < 4) K = 4;
+  if (K > 32) K = 32;
+  // large n: buckets average entries / nbt > 32 entries; a chunk of about one average bucket keeps
+  // most crossing buckets at two pieces (joined inside k_accumulate), capped at 256 entries so the
+  // grid still has many rounds of waves (swept, tools/gpu_sweep_big.sh: 2^21 K = 64 4.47 -> 4.41 ms;
+  // 2^24 K = 256 32.0 ms, 512 32.4, 1024 33.4)
+  const uint64_t avg_bucket = entries / nbt;
+  if (K < avg_bucket) K = avg_bucket < 256 ? avg_bucket : 256;
+  if (const char* e = getenv("SVGPU_ACC_K")) K = (uint64_t)atoi(e);
+  if (K < 1) K = 1;
+  return (uint32_t)K;
+}
+
 MsmPlan msm_plan(size_t n) {
   MsmPlan p;
   // GLV (k P = k1 P + k2 phi(P), 128-bit halves, split on the fly by the sort passes) halves the
@@ -928,18 +962,7 @@ MsmPlan msm_plan(size_t n) {
   p.B = 1u << (c - 1);
   p.nbt = p.B * p.W;
   uint64_t entries = (uint64_t)p.npts * p.W;
-  uint64_t K = entries / (1u << 18);
-  if (K < 4) K = 4;
-  if (K > 32) K = 32;
-  // large n: buckets average entries / nbt > 32 entries; a chunk of about one average bucket keeps
-  // most crossing buckets at two pieces (joined inside k_accumulate), capped at 256 entries so the
-  // grid still has many rounds of waves (swept, tools/gpu_sweep_big.sh: 2^21 K = 64 4.47 -> 4.41 ms;
-  // 2^24 K = 256 32.0 ms, 512 32.4, 1024 33.4)
-  const uint64_t avg_bucket = entries / p.nbt;
-  if (K < avg_bucket) K = avg_bucket < 256 ? avg_bucket : 256;
-  if (const char* e = getenv("SVGPU_ACC_K")) K = (uint64_t)atoi(e);
-  if (K < 1) K = 1;
-  p.K = (uint32_t)K;
+  p.K = plan_K(entries, p.nbt);
   p.T = cdiv(entries, p.K);
   // reduction: J running-sum segments per window, NG subset groups of H = J/2 points
   // 8 buckets per running-sum segment (swept: tools/gpu_sweep_red.sh); 4 with GLV, whose W / 2
@@ -1019,20 +1042,28 @@ static host::Xyzz host_combine(const MsmPlan& p, const host::Xyzz* A) {
   return acc;
 }
 
-// One piece's front half: digits + two-level sort + bucket accumulation + crossing-bucket fixups
-// of points [0, m) of (bases, scalars) into bsum (complete buckets only; emptiness from gst).
+// Scratch of the sort / accumulate stages.  The sort's own buffers (bcnt, btot, bstart, tmp) are
+// reused piece after piece on one stream; its outputs (SortOut) and the accumulate's crossing-bucket
+// pieces and queues are per piece / per accumulate stream.
 struct MsmScratch {
-  uint32_t *err, *bcnt, *btot, *bstart, *gst, *ent, *tstart, *heavy, *multi, *nheavy, *nmulti;
+  uint32_t *err, *bcnt, *btot, *bstart, *heavy, *multi, *nheavy, *nmulti;
   uint64_t* tmp;
   G1Xyzz *pfirst, *plast;
 };
+struct SortOut {
+  uint32_t* ent;     // the piece's sorted entries (virtual point | sign << 31)
+  uint32_t* gst;     // bucket starts, nbt + 1 (gst[nbt] = the entry total)
+  uint32_t* tstart;  // owner bucket of every accumulate chunk
+  uint32_t K, T;     // entries per accumulate thread, accumulate threads
+};
 
-static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, const Fr* scalars, size_t m,
-                     int mont_in, int device, hipStream_t st, G1Xyzz* bsum, const uint4* phix, uint32_t nsplit,
-                     hipEvent_t ev_sorted, hipEvent_t ev_sort_mid, hipEvent_t ev_acc_done, hipEvent_t ev_fix_mid,
-                     hipEvent_t bases_ready, const G1Aff* conv_src, hipStream_t side = nullptr,
-                     hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr,
-                     const std::function<int()>& stage_bases = nullptr) {
+// Digits + two-level counting sort of points [0, m) (virtual points i and, with GLV, nsplit + i)
+// into so, on stream st.  With phix set (bases resident) k_bin_hist also writes the GLV table;
+// check_bases: Montgomery bases checked to be reduced on the way.
+static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, const G1Aff* bases,
+                    const Fr* scalars, size_t m, int mont_in, int device, hipStream_t st, uint4* phix,
+                    uint32_t nsplit, int check_bases, hipEvent_t ev_sort_mid, hipStream_t side = nullptr,
+                    hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr) {
   const int LOGB = p.c - 1;
   const int nb = p.glv ? 128 : 255;
   const uint32_t CB = (uint32_t)coarse_bits(p.c, nb), FB = (uint32_t)LOGB - CB, NBIN = 1u << CB;
@@ -1040,17 +1071,16 @@ static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, 
   const uint32_t npts = (uint32_t)m;  // real points (GLV: 2 m virtual ones)
   const uint32_t ep = p.glv ? 2 * p.W : p.W;
   const uint32_t nblk = cdiv(npts, sort_chunk((int)ep));
-  const uint32_t T = cdiv((uint64_t)npts * ep, p.K);
   // u32 entries when every virtual point index (below nsplit + m with GLV, m without) fits
   const uint64_t vmax = p.glv ? (uint64_t)nsplit + npts : (uint64_t)npts;
   int e32 = vmax <= (uint64_t(1) << (31 - FB)) ? 1 : 0;
   if (const char* e = getenv("SVGPU_SORT_E32")) e32 = e32 && atoi(e) != 0;
   SV_LAUNCH_C(k_bin_hist, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.err, bases,
-              bases_ready ? nullptr : const_cast<uint4*>(phix), p.phi64);
+              phix, p.phi64, check_bases);
   SV_HIP(hipGetLastError());
   if (ev_sort_mid) SV_HIP(hipEventRecord(ev_sort_mid, st));
   hipLaunchKernelGGL(k_bin_scan_chunks, dim3(nwb), dim3(kBlock), 0, st, w.bcnt, nblk, w.btot);
-  hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, w.btot, nwb, w.bstart, w.gst + p.nbt);
+  hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, w.btot, nwb, w.bstart, so.gst + p.nbt);
   SV_LAUNCH_C(k_bin_scatter, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.btot, w.bstart,
               w.tmp, e32);
   static thread_local int fine_attr_dev = -1;  // the > 64 KiB dynamic-LDS opt-in, once per thread/device
@@ -1068,34 +1098,87 @@ static int msm_front(const MsmPlan& p, const MsmScratch& w, const G1Aff* bases, 
     SV_HIP(hipEventRecord(ev_fork, st));
     SV_HIP(hipStreamWaitEvent(side, ev_fork, 0));
   }
-  hipLaunchKernelGGL(k_fine_sort<true>, dim3(nwb), dim3(1024), kFineLds, big_st, w.tmp, e32, w.bstart, FB, p.K,
-                     w.gst, w.tstart, w.ent);
-  hipLaunchKernelGGL(k_fine_sort<false>, dim3(nwb), dim3(1024), kFineLds, st, w.tmp, e32, w.bstart, FB, p.K, w.gst,
-                     w.tstart, w.ent);
+  hipLaunchKernelGGL(k_fine_sort<true>, dim3(nwb), dim3(1024), kFineLds, big_st, w.tmp, e32, w.bstart, FB, so.K,
+                     so.gst, so.tstart, so.ent);
+  hipLaunchKernelGGL(k_fine_sort<false>, dim3(nwb), dim3(1024), kFineLds, st, w.tmp, e32, w.bstart, FB, so.K, so.gst,
+                     so.tstart, so.ent);
   if (side) {
     SV_HIP(hipEventRecord(ev_join, side));
     SV_HIP(hipStreamWaitEvent(st, ev_join, 0));
   }
   SV_HIP(hipGetLastError());
-  if (stage_bases) SV_TRY(stage_bases());  // host-fed: the bases' transfer, after the sort is queued
-  if (bases_ready) SV_HIP(hipStreamWaitEvent(st, bases_ready, 0));
-  if (conv_src)  // host-fed canonical bases: converted once they have landed, after the sort
-    hipLaunchKernelGGL(k_to_mont_bases, dim3(cdiv(npts, kBlock)), dim3(kBlock), 0, st, conv_src,
-                       const_cast<G1Aff*>(bases), npts, w.err);
-  if (bases_ready && p.glv)  // host-fed GLV piece: its phi table from the landed (converted) bases
-    hipLaunchKernelGGL(k_glv_phix, dim3(cdiv(npts, kBlock)), dim3(kBlock), 0, st, bases, npts,
-                       const_cast<uint4*>(phix), p.phi64);
-  if (ev_sorted) SV_HIP(hipEventRecord(ev_sorted, st));
-  hipLaunchKernelGGL(k_accumulate, dim3(cdiv(T, kBlock)), dim3(kBlock), 0, st, bases, w.ent, w.gst, w.tstart,
-                     p.nbt, p.K, T, bsum, w.pfirst, w.plast, w.multi, w.nmulti, w.heavy, w.nheavy, phix, nsplit, p.phi64);
+  return SV_OK;
+}
+
+// Bucket accumulation of a sorted piece + its crossing-bucket fixups into bsum, on stream st
+// (add_into: the piece's bucket sums are added to what bsum holds; otherwise complete buckets are
+// stored and empty ones left untouched).
+static int msm_acc(const MsmPlan& p, const MsmScratch& w, const SortOut& so, const G1Aff* bases, int add_into,
+                   hipStream_t st, G1Xyzz* bsum, const uint4* phix, uint32_t nsplit, hipEvent_t ev_acc_done,
+                   hipEvent_t ev_fix_mid) {
+  if (add_into)
+    hipLaunchKernelGGL(k_accumulate<true>, dim3(cdiv(so.T, kBlock)), dim3(kBlock), 0, st, bases, so.ent, so.gst,
+                       so.tstart, p.nbt, so.K, so.T, bsum, w.pfirst, w.plast, w.multi, w.nmulti, w.heavy, w.nheavy,
+                       phix, nsplit, p.phi64);
+  else
+    hipLaunchKernelGGL(k_accumulate<false>, dim3(cdiv(so.T, kBlock)), dim3(kBlock), 0, st, bases, so.ent, so.gst,
+                       so.tstart, p.nbt, so.K, so.T, bsum, w.pfirst, w.plast, w.multi, w.nmulti, w.heavy, w.nheavy,
+                       phix, nsplit, p.phi64);
   SV_HIP(hipGetLastError());
   if (ev_acc_done) SV_HIP(hipEventRecord(ev_acc_done, st));
   const uint32_t gm = std::min<uint32_t>(cdiv(p.nbt, kBlock), 1024);
-  hipLaunchKernelGGL(k_fixup, dim3(gm + 256), dim3(kBlock), 0, st, w.gst, p.K, w.pfirst, w.plast, w.multi, w.nmulti,
-                     w.heavy, w.nheavy, gm, bsum);
+  if (add_into)
+    hipLaunchKernelGGL(k_fixup<true>, dim3(gm + 256), dim3(kBlock), 0, st, so.gst, so.K, w.pfirst, w.plast, w.multi,
+                       w.nmulti, w.heavy, w.nheavy, gm, bsum);
+  else
+    hipLaunchKernelGGL(k_fixup<false>, dim3(gm + 256), dim3(kBlock), 0, st, so.gst, so.K, w.pfirst, w.plast, w.multi,
+                       w.nmulti, w.heavy, w.nheavy, gm, bsum);
   SV_HIP(hipGetLastError());
   if (ev_fix_mid) SV_HIP(hipEventRecord(ev_fix_mid, st));
   return SV_OK;
+}
+
+// Host-fed piece boundaries: SVGPU_H2D_SPLIT = comma-separated weights, else `pieces` equal pieces
+// (SVGPU_H2D_PIECES), else the default schedule.  The host-fed MSM is transfer-bound (96 B per point
+// at ~54 GB/s) and a piece's accumulate runs only once its bases have landed, so the schedule starts
+// with small pieces (the accumulate starts early) and ends with a small one (little work left after
+// the last byte lands); in between, pieces are large enough to keep each accumulate efficient.
+static std::vector<size_t> piece_bounds(size_t n, int pieces) {
+  std::vector<double> wts;
+  if (const char* e = getenv("SVGPU_H2D_SPLIT")) {
+    for (const char* q = e; *q;) {
+      char* end = nullptr;
+      const double v = strtod(q, &end);
+      if (end == q) break;
+      if (v > 0) wts.push_back(v);
+      q = *end == ',' ? end + 1 : end;
+      if (*end && *end != ',') break;
+    }
+  }
+  if (wts.empty()) {
+    if (pieces > 0) {
+      wts.assign(std::min(pieces, 16), 1.0);
+    } else if (n >= (size_t(1) << 18)) {
+      wts = {2, 2, 3, 3, 3, 3};
+    } else if (n >= (size_t(1) << 15)) {
+      wts = {1, 1};
+    } else {
+      wts = {1};
+    }
+  }
+  if (wts.size() > 16) wts.resize(16);
+  // pieces below 4096 points are not worth a launch sequence
+  while (wts.size() > 1 && n < wts.size() * 4096) wts.pop_back();
+  double tot = 0;
+  for (double v : wts) tot += v;
+  std::vector<size_t> b{0};
+  double cum = 0;
+  for (size_t k = 0; k + 1 < wts.size(); k++) {
+    cum += wts[k];
+    b.push_back(std::max(b.back(), std::min(n, (size_t)((double)n * cum / tot))));
+  }
+  b.push_back(n);
+  return b;
 }
 
 static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, int form, int device,
@@ -1116,27 +1199,31 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   if (!lease.ok()) return SV_ERR_DEVICE;
   Workspace* ws = lease.get();
   hipStream_t st = ws->stream;
-  // host-fed inputs arrive in pieces: piece k's sort + accumulate run while piece k + 1 is in flight
   MsmPlan p = msm_plan(n);
-  int pieces = 1;
-  if (feed) {
-    // default: 2 pieces with GLV, 4 without (tools/host_api_bench.py at 2^20: GLV 3.17 ms with 2,
-    // 3.34 with 4 -- each piece's accumulate over a quarter of the points runs at ~70 % of the whole
-    // one's rate; no GLV 3.34 / 3.25)
-    pieces = feed->pieces > 0 ? feed->pieces : (p.glv ? 2 : 4);
-    if (n < (size_t)pieces * 4096) pieces = 1;
-    if (pieces > 8) pieces = 8;
-  }
-  const size_t max_piece = (n + pieces - 1) / pieces;
+  // host-fed inputs arrive in pieces (piece_bounds): piece k is sorted on the sort stream once its
+  // scalars have landed and accumulated on the compute stream once its bases have, while later
+  // pieces are still in flight
+  const std::vector<size_t> pb = feed ? piece_bounds(n, feed->pieces) : std::vector<size_t>{0, n};
+  const int pieces = (int)pb.size() - 1;
   const uint32_t ep = p.glv ? 2 * p.W : p.W;  // entries per real point
-  const uint64_t entries = (uint64_t)max_piece * ep;  // per piece
-  const uint32_t Tmax = cdiv(entries, p.K);
+  size_t max_piece = 0;
+  uint64_t tst_total = 0;
+  uint32_t Tmax = 0;
+  std::vector<SortOut> so(pieces);
+  for (int k = 0; k < pieces; k++) {
+    const uint64_t e = (uint64_t)(pb[k + 1] - pb[k]) * ep;
+    max_piece = std::max(max_piece, pb[k + 1] - pb[k]);
+    so[k].K = feed ? plan_K(e, p.nbt) : p.K;  // each piece's chunk length for its own size
+    so[k].T = cdiv(e, so[k].K);
+    tst_total += (uint64_t)so[k].T + 1;
+    Tmax = std::max(Tmax, so[k].T);
+  }
+  const uint64_t entries = (uint64_t)n * ep;              // all pieces
+  const uint64_t piece_entries = (uint64_t)max_piece * ep;  // the sort scratch, reused per piece
 
-  // ---- workspace layout (sort / accumulate scratch sized for the largest piece)
-  const int LOGB = p.c - 1;
+  // ---- workspace layout
   const int nb = p.glv ? 128 : 255;
   const uint32_t CB = (uint32_t)coarse_bits(p.c, nb), NBIN = 1u << CB;
-  (void)LOGB;
   const uint32_t nwb = p.W * NBIN;
   const uint32_t nblk = cdiv(max_piece, sort_chunk((int)ep));
   size_t bytes = 0;
@@ -1153,18 +1240,14 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   add((size_t)nwb * nblk * 4);                // bcnt
   add((size_t)nwb * 4);                       // btot
   add(((size_t)nwb + 1) * 4);                 // bstart
-  add(entries * 8);                           // tmp (coarse-binned entries)
-  add(((size_t)p.nbt + 1) * 4);               // gst
-  add(entries * 4);                           // ent
-  add(((size_t)Tmax + 1) * 4);                // tstart
+  add(piece_entries * 8);                     // tmp (coarse-binned entries)
+  add(((size_t)p.nbt + 1) * 4 * pieces);      // gst per piece
+  add(entries * 4);                           // ent (every piece's sorted entries)
+  add(tst_total * 4);                         // tstart per piece
   add((size_t)Tmax * sizeof(G1Xyzz) * 2);     // pfirst, plast
   add((size_t)p.nbt * sizeof(G1Xyzz));        // bsum
   add((size_t)p.nbt * 4);                     // heavy-bucket queue
   add((size_t)p.nbt * 4);                     // multi-thread-bucket queue
-  if (pieces > 1) {
-    add((size_t)p.nbt * sizeof(G1Xyzz));      // bsum of pieces 1..
-    add(((size_t)p.nbt + 1) * 4);             // gst of piece 0
-  }
   add((size_t)p.J * p.W * sizeof(G1Xyzz) * 2);  // acc_j, T_j
   add(nfinal * sizeof(G1Xyzz));                 // group sums
   add(nfinal * gparts * sizeof(G1Xyzz));        // group slice sums
@@ -1173,6 +1256,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   if (feed) {
     SV_TRY(ws->reserve_in(Workspace::aligned(n * sizeof(G1Aff)) + Workspace::aligned(n * sizeof(Fr))));
     SV_TRY(ws->ensure_copy_stream());
+    SV_TRY(ws->ensure_sort_stream());
     d_bases = ws->inbuf;
     d_scalars = ws->inbuf + Workspace::aligned(n * sizeof(G1Aff));
   }
@@ -1189,10 +1273,10 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   w.bcnt = ws->carve<uint32_t>((size_t)nwb * nblk);
   w.btot = ws->carve<uint32_t>(nwb);
   w.bstart = ws->carve<uint32_t>((size_t)nwb + 1);
-  w.tmp = ws->carve<uint64_t>(entries);
-  w.gst = ws->carve<uint32_t>((size_t)p.nbt + 1);
-  w.ent = ws->carve<uint32_t>(entries);
-  w.tstart = ws->carve<uint32_t>((size_t)Tmax + 1);
+  w.tmp = ws->carve<uint64_t>(piece_entries);
+  uint32_t* gst_all = ws->carve<uint32_t>(((size_t)p.nbt + 1) * pieces);
+  uint32_t* ent_all = ws->carve<uint32_t>(entries);
+  uint32_t* tst_all = ws->carve<uint32_t>(tst_total);
   w.pfirst = ws->carve<G1Xyzz>(Tmax);
   w.plast = ws->carve<G1Xyzz>(Tmax);
   G1Xyzz* bsum = ws->carve<G1Xyzz>(p.nbt);
@@ -1200,11 +1284,19 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   w.multi = ws->carve<uint32_t>(p.nbt);
   w.nheavy = w.err + 1;  // zeroed with the error flag
   w.nmulti = w.err + 2;
-  G1Xyzz* bsum_k = pieces > 1 ? ws->carve<G1Xyzz>(p.nbt) : nullptr;
-  uint32_t* gst0 = pieces > 1 ? ws->carve<uint32_t>((size_t)p.nbt + 1) : nullptr;
   G1Xyzz* racc = ws->carve<G1Xyzz>((size_t)p.J * p.W);
   G1Xyzz* rtot = ws->carve<G1Xyzz>((size_t)p.J * p.W);
   G1Xyzz* gpart = ws->carve<G1Xyzz>(nfinal * gparts);
+  {
+    uint64_t eo = 0, to = 0;
+    for (int k = 0; k < pieces; k++) {
+      so[k].ent = ent_all + eo;
+      so[k].gst = gst_all + (size_t)k * (p.nbt + 1);
+      so[k].tstart = tst_all + to;
+      eo += (uint64_t)(pb[k + 1] - pb[k]) * ep;
+      to += (uint64_t)so[k].T + 1;
+    }
+  }
 
   hipEvent_t* ev = ws->ev;
   // each event record between kernels costs ~5.5 us of idle GPU (rocprof trace): the accumulate is
@@ -1216,6 +1308,15 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   const bool detail = detail_env && !lean;
   const char* fork_env = getenv("SVGPU_SORT_FORK");
   const bool fork_sort = fork_env && atoi(fork_env) != 0;  // off: measured slower (the join delays the accumulate)
+  // a host-fed call that fails part-way leaves copies (and sorts) queued on its other streams: drain
+  // them before the lease returns the staging buffers to the pool
+  struct Drain {
+    Workspace* ws;
+    bool armed;
+    ~Drain() {
+      if (armed) (void)ws->quiesce();
+    }
+  } drain{ws, feed != nullptr};
   if (!lean) SV_HIP(hipEventRecord(ev[0], st));
   SV_HIP(hipMemsetAsync(w.err, 0, nerr * 4, st));
   if (!feed) {
@@ -1229,55 +1330,67 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
       SV_TRY(ws->ensure_copy_stream());  // idle on the device path
       side = ws->copy_stream;
     }
-    SV_TRY(msm_front(p, w, bases, scalars, n, mont_in, device, st, bsum, phix, p.glv ? (uint32_t)n : ~0u, ev[2],
-                     detail ? ev[1] : nullptr, ev[3], detail ? ev[4] : nullptr, nullptr, nullptr, side, ev[24],
-                     ev[25]));
+    const uint32_t nsplit = p.glv ? (uint32_t)n : ~0u;
+    SV_TRY(msm_sort(p, w, so[0], bases, scalars, n, mont_in, device, st, phix, nsplit, mont_in,
+                    detail ? ev[1] : nullptr, side, ev[60], ev[61]));
+    SV_HIP(hipEventRecord(ev[2], st));
+    SV_TRY(msm_acc(p, w, so[0], bases, 0, st, bsum, phix, nsplit, ev[3], detail ? ev[4] : nullptr));
   } else {
-    // Piece k: the copy stream stages its scalars, then its bases; the compute stream sorts the
-    // piece once its scalars have landed and accumulates it once its bases have (k_to_mont_bases
-    // first for canonical input).  Pieces >= 1 are merged into piece 0's bucket sums.
-    hipStream_t cs = ws->copy_stream;
+    // Piece k: the copy stream stages its scalars, then its bases (the pageable copy blocks this
+    // thread, so the piece's sort is queued in between and runs during the base transfer); the sort
+    // stream sorts the piece once its scalars have landed, beside the previous piece's accumulate;
+    // the compute stream converts / checks the landed bases, writes the piece's GLV table and
+    // accumulates the piece into the one bucket set (identity-initialised; pieces after the first
+    // add into it).
+    hipStream_t cs = ws->copy_stream, ss = ws->sort_stream;
+    if (pieces > 1) SV_HIP(hipMemsetAsync(bsum, 0, (size_t)p.nbt * sizeof(G1Xyzz), st));
     SV_HIP(hipEventRecord(ev[6], st));
-    SV_HIP(hipStreamWaitEvent(cs, ev[6], 0));  // the previous call's readers of inbuf are done
+    SV_HIP(hipStreamWaitEvent(cs, ev[6], 0));
+    SV_HIP(hipStreamWaitEvent(ss, ev[6], 0));
     for (int k = 0; k < pieces; k++) {
-      const size_t lo = n * k / pieces, hi = n * (k + 1) / pieces, m = hi - lo;
-      hipEvent_t sc_ready = ws->ev[8 + 2 * k], b_ready = ws->ev[9 + 2 * k];
-      G1Aff* db = const_cast<G1Aff*>(reinterpret_cast<const G1Aff*>(d_bases)) + lo;
+      const size_t lo = pb[k], hi = pb[k + 1], m = hi - lo;
+      hipEvent_t sc_ready = ev[8 + 3 * k], b_ready = ev[9 + 3 * k], sorted = ev[10 + 3 * k];
+      G1Aff* db = const_cast<G1Aff*>(bases) + lo;
       Fr* dsc = const_cast<Fr*>(scalars) + lo;
-      SV_TRY(feed->stage_scalars(lo, hi, dsc, cs, sc_ready));
-      SV_HIP(hipStreamWaitEvent(st, sc_ready, 0));
-      const std::function<int()> stage_b = [&]() { return feed->stage_bases(lo, hi, db, cs, b_ready); };
-      if (k > 0) SV_HIP(hipMemsetAsync(w.err + 1, 0, 8, st));  // fixup queue counters
-      const G1Aff* pb = conv ? bases_m + lo : db;
-      G1Xyzz* dst = k == 0 ? bsum : bsum_k;
       // GLV: piece-local virtual points (i, m + i) over the piece's bases and its slice of the table
+      const uint32_t nsplit = p.glv ? (uint32_t)m : ~0u;
       uint4* phix_k = p.glv ? phix + (size_t)(p.phi64 ? 4 : 2) * lo : nullptr;
-      SV_TRY(msm_front(p, w, pb, dsc, m, mont_in, device, st, dst, phix_k, p.glv ? (uint32_t)m : ~0u,
-                       k == 0 ? ev[2] : nullptr, nullptr, k == pieces - 1 ? ev[3] : nullptr, nullptr, b_ready,
-                       conv ? db : nullptr, nullptr, nullptr, nullptr, stage_b));
-      if (pieces > 1) {
-        if (k == 0) {
-          SV_HIP(hipMemcpyAsync(gst0, w.gst, ((size_t)p.nbt + 1) * 4, hipMemcpyDeviceToDevice, st));
-        } else {
-          hipLaunchKernelGGL(k_merge_buckets, dim3(cdiv(p.nbt, kBlock)), dim3(kBlock), 0, st, bsum,
-                             k == 1 ? gst0 : nullptr, bsum_k, w.gst, p.nbt);
-          SV_HIP(hipGetLastError());
-        }
-      }
+      SV_TRY(feed->stage_scalars(lo, hi, dsc, cs, sc_ready));
+      SV_HIP(hipStreamWaitEvent(ss, sc_ready, 0));
+      SV_TRY(msm_sort(p, w, so[k], nullptr, dsc, m, mont_in, device, ss, nullptr, nsplit, 0, nullptr));
+      SV_HIP(hipEventRecord(sorted, ss));
+      SV_TRY(feed->stage_bases(lo, hi, db, cs, b_ready));
+      SV_HIP(hipStreamWaitEvent(st, b_ready, 0));
+      const G1Aff* pbases = conv ? bases_m + lo : db;
+      if (conv)  // canonical bases converted (and checked) once they have landed
+        hipLaunchKernelGGL(k_to_mont_bases, dim3(cdiv(m, kBlock)), dim3(kBlock), 0, st, db, bases_m + lo,
+                           (uint32_t)m, w.err);
+      else if (!p.glv)
+        hipLaunchKernelGGL(k_check_bases, dim3(cdiv(m, kBlock)), dim3(kBlock), 0, st, db, (uint32_t)m, w.err);
+      if (p.glv)  // the piece's phi table from the landed (converted) bases; Montgomery ones checked
+        hipLaunchKernelGGL(k_glv_phix, dim3(cdiv(m, kBlock)), dim3(kBlock), 0, st, pbases, (uint32_t)m, phix_k,
+                           p.phi64, conv ? nullptr : w.err);
+      SV_HIP(hipGetLastError());
+      SV_HIP(hipStreamWaitEvent(st, sorted, 0));
+      if (k > 0) SV_HIP(hipMemsetAsync(w.err + 1, 0, 8, st));  // fixup queue counters
+      if (k == 0) SV_HIP(hipEventRecord(ev[2], st));
+      SV_TRY(msm_acc(p, w, so[k], pbases, k > 0 ? 1 : 0, st, bsum, phix_k, nsplit,
+                     k == pieces - 1 ? ev[3] : nullptr, nullptr));
     }
   }
-  // bucket reduction: running sums over segments of 2^logL buckets, then the subset sums (after a
-  // piece merge every bucket of bsum is written: no emptiness table).  (Reducing the top windows
+  // bucket reduction: running sums over segments of 2^logL buckets, then the subset sums (with
+  // several host-fed pieces every bucket of bsum holds a value: no emptiness table).  (Reducing the top windows
   // first to overlap the host Horner with the lower ones was measured slower: each half-size launch
   // of these occupancy-bound kernels takes nearly as long as the whole -- reduce 0.40 -> 0.67 ms.)
   hipLaunchKernelGGL(k_wsum, dim3(cdiv((uint64_t)p.J * p.W, kBlock)), dim3(kBlock), 0, st, bsum,
-                     pieces > 1 ? nullptr : w.gst, p.B, p.J, 1u << p.logL, p.W, 1, racc, rtot);
+                     pieces > 1 ? nullptr : so[0].gst, p.B, p.J, 1u << p.logL, p.W, 1, racc, rtot);
   hipLaunchKernelGGL(k_group_sum, dim3(p.NG * p.W * gparts), dim3(kGroupBlock), 0, st, racc, rtot, p.J, p.logJ,
                      gparts, ping, gpart, w.err + 64);
   SV_HIP(hipGetLastError());
   if (!lean) SV_HIP(hipEventRecord(ev[5], st));
   SV_HIP(hipMemcpyAsync(ws->pinned, ping, nfinal * sizeof(G1Xyzz) + 4, hipMemcpyDeviceToHost, st));
   SV_HIP(hipStreamSynchronize(st));
+  drain.armed = false;  // the copy and sort streams' work all precedes the compute stream's end
   uint32_t errv;
   memcpy(&errv, ws->pinned + nfinal * sizeof(G1Xyzz), 4);
   if (errv) {

@@ -33,7 +33,7 @@ int Workspace::reserve(size_t bytes) {
   if (bytes <= cap) return SV_OK;
   SV_HIP(hipSetDevice(device));
   if (buf) {
-    SV_HIP(hipStreamSynchronize(stream));
+    SV_TRY(quiesce());
     SV_HIP(hipFree(buf));
     buf = nullptr;
     cap = 0;
@@ -98,6 +98,14 @@ int Workspace::quiesce() {
   SV_HIP(hipSetDevice(device));
   if (stream) SV_HIP(hipStreamSynchronize(stream));
   if (copy_stream) SV_HIP(hipStreamSynchronize(copy_stream));
+  if (sort_stream) SV_HIP(hipStreamSynchronize(sort_stream));
+  return SV_OK;
+}
+
+int Workspace::ensure_sort_stream() {
+  if (sort_stream) return SV_OK;
+  SV_HIP(hipSetDevice(device));
+  SV_HIP(hipStreamCreateWithFlags(&sort_stream, hipStreamNonBlocking));
   return SV_OK;
 }
 

@@ -35,7 +35,8 @@ struct Workspace {
   char* stage = nullptr;
   size_t stage_cap = 0;
   hipStream_t copy_stream = nullptr;
-  static constexpr int kEvents = 26;
+  hipStream_t sort_stream = nullptr;  // host-fed MSM: piece k + 1's sort beside piece k's accumulate
+  static constexpr int kEvents = 64;
   hipEvent_t ev[kEvents] = {};
 
 
@@ -53,6 +54,7 @@ struct Workspace {
   int reserve_in(size_t bytes);      // grow-only device input buffer
   int reserve_stage(size_t bytes);   // grow-only pinned gather staging
   int ensure_copy_stream();
+  int ensure_sort_stream();
   int quiesce();  // wait for the compute and copy streams (before freeing or reusing staging)
 };
 

@@ -37,14 +37,20 @@ B = Bd.cpu().numpy().view(np.uint64).copy()
 S = Sd.cpu().numpy().view(np.uint64).copy()
 dms, ref = t(lambda: (dv.msm(Bd, Sd, M), torch.cuda.synchronize())[0])
 print(f"device-resident  {dms:7.3f} ms")
-for glv in ("1", "0"):
-    os.environ["SVGPU_GLV"] = glv
-    for p in ("1", "2", "4", "6", "8"):
-        os.environ["SVGPU_H2D_PIECES"] = p
-        ms, r = t(lambda: svgpu.msm_arrays(B, S, M))
-        print(f"host glv={glv} pieces={p}    {ms:7.3f} ms  x{ms / dms:.2f}  ok={r == ref}")
-os.environ.pop("SVGPU_GLV")
-os.environ["SVGPU_H2D_PIECES"] = "4"
+specs = sys.argv[2:] or ["", "SVGPU_H2D_PIECES=1", "SVGPU_H2D_PIECES=2", "SVGPU_H2D_PIECES=4",
+                         "SVGPU_H2D_PIECES=6", "SVGPU_H2D_PIECES=8", "SVGPU_H2D_SPLIT=1,1,2,3,3,3,3",
+                         "SVGPU_H2D_SPLIT=1,2,3,3,3,2", "SVGPU_H2D_SPLIT=2,3,3,3,3,2",
+                         "SVGPU_H2D_SPLIT=1,2,2,3,3,3,2"]
+for spec in specs:
+    for k in ("SVGPU_H2D_PIECES", "SVGPU_H2D_SPLIT", "SVGPU_GLV"):
+        os.environ.pop(k, None)
+    for kv in filter(None, spec.split(" ")):
+        k, v = kv.split("=")
+        os.environ[k] = v
+    ms, r = t(lambda: svgpu.msm_arrays(B, S, M))
+    print(f"host [{spec or 'default'}]  {ms:7.3f} ms  x{ms / dms:.2f}  ok={r == ref}", flush=True)
+for k in ("SVGPU_H2D_PIECES", "SVGPU_H2D_SPLIT", "SVGPU_GLV"):
+    os.environ.pop(k, None)
 rng = np.random.default_rng(1)
 perm = rng.permutation(n)
 sp = S.ctypes.data + 32 * perm.astype(np.uint64)

@@ -125,10 +125,16 @@ def next_rows(dev, dv, ob, enc, g2, sg2, accs):
     return res
 
 
+def affinity_cores() -> int:
+    """Cores this process may run on (sched_getaffinity): what rayon's default pool would use for
+    the reference's `parallel` Pippenger (util.rs:83-152, msm.rs:290-310)."""
+    return len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+
+
 def cpu_threads() -> int:
     """Host threads for the CPU legs: every core this process may run on, capped by the box's
     OMP_NUM_THREADS share when that is set (one GPU's slice of a shared node)."""
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cores = affinity_cores()
     share = os.environ.get("OMP_NUM_THREADS")
     return min(cores, int(share)) if share and share.isdigit() and int(share) > 0 else cores
 
@@ -158,6 +164,14 @@ def cpu_baseline(args, n, gpu_result, g2, sg2, accs, enc):
     cpu_res = cpu_ref.msm_pippenger(hb, hs, threads)
     cpu_s = time.perf_counter() - t0
     parity = ob.g1_from_bytes(cpu_res.tobytes()) == gpu_result
+    # the same port on every core the affinity mask allows (rayon's default would take them all)
+    aff = affinity_cores()
+    aff_s = None
+    if aff != threads:
+        t0 = time.perf_counter()
+        aff_res = cpu_ref.msm_pippenger(hb, hs, aff)
+        aff_s = time.perf_counter() - t0
+        parity = parity and ob.g1_from_bytes(aff_res.tobytes()) == gpu_result
     naive = {}
     for lg in (10, 12):
         m = 1 << lg
@@ -196,6 +210,9 @@ def cpu_baseline(args, n, gpu_result, g2, sg2, accs, enc):
                   "config 5: accumulate 64 + one decide on 1 thread" % (args.log_n, threads, ds, len(accs), threads),
         "cpu_model": cpu_model(),
         "host_cpus_visible": os.cpu_count(),
+        "affinity_cores": aff,
+        "threads_note": "cores = min(affinity cores, OMP_NUM_THREADS share of this GPU's box slice)",
+        "value_affinity_cores": n / aff_s if aff_s else n / cpu_s,
         "seconds": cpu_s,
         "parity_vs_gpu": bool(parity and cff == -1 and aff == -1 and c5ff == -1),
         "naive_nativeloader": {

@@ -33,7 +33,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <functional>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "curve.hpp"
@@ -624,13 +627,6 @@ __device__ __forceinline__ bool join_in_block(uint32_t gs, uint32_t ge, uint32_t
   const uint32_t t0 = gs / K, t1 = (ge - 1) / K;
   return t1 == t0 + 1 && t0 / kBlock == t1 / kBlock;
 }
-// A complete bucket sum: stored, or (ADD: host-fed pieces after the first, into a bucket set that
-// started as all identity) added to the sum the earlier pieces left there.
-template <bool ADD>
-__device__ __forceinline__ void bucket_put(G1Xyzz* __restrict__ bsum, uint32_t g, const G1Xyzz& v) {
-  if constexpr (ADD) store_xyzz(bsum, g, xyzz_add(v, load_xyzz(bsum, g)));
-  else store_xyzz(bsum, g, v);
-}
 template <bool ADD>
 __global__ void __launch_bounds__(kBlock) k_accumulate(
     const G1Aff* __restrict__ bases, const uint32_t* __restrict__ ent, const uint32_t* __restrict__ gst,
@@ -654,6 +650,12 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
     ge = gst[g + 1];
     uint32_t seg_start = s0;
     bool first = true;
+    // ADD (host-fed pieces after the first): a segment that starts its bucket -- the owner piece --
+    // starts from the sum the earlier pieces left in bsum (identity-initialised) instead of the
+    // identity, so every later join (in block, k_fixup) and store carries it: no extra addition
+    if constexpr (ADD) {
+      if (s0 == gs) acc = load_xyzz(bsum, g);
+    }
 #if SV_ACC_PREFETCH >= 1
     uint32_t vnext = ent[s0];
 #endif
@@ -668,7 +670,7 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
       if (e >= ge) {  // segment [seg_start, ge) of bucket g ends inside this chunk
         acc = xyzz_canon2p(acc);
         if (seg_start == gs) {
-          bucket_put<ADD>(bsum, g, acc);
+          store_xyzz(bsum, g, acc);
         } else {  // head piece of a bucket owned by an earlier thread
           if (join_in_block(gs, ge, K)) shead[threadIdx.x] = acc;
           else store_xyzz(pfirst, t, acc);
@@ -680,7 +682,9 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
           ge = gst[g + 1];
         } while (ge <= e);
         seg_start = e;
-        acc = G1Xyzz::identity();
+        // the new segment starts bucket g (gs == e: entries are contiguous, empty buckets skipped)
+        if constexpr (ADD) acc = load_xyzz(bsum, g);
+        else acc = G1Xyzz::identity();
       }
 #if SV_ACC_PREFETCH == 0
       const uint32_t v = ent[e], idx = v & 0x7fffffffu;
@@ -703,7 +707,7 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
     }
     acc = xyzz_canon2p(acc);
     if (seg_start == gs && e_end == ge) {
-      bucket_put<ADD>(bsum, g, acc);
+      store_xyzz(bsum, g, acc);
     } else if (seg_start != gs) {  // first segment, bucket started earlier (it may also go on later)
       if (join_in_block(gs, ge, K)) shead[threadIdx.x] = acc;
       else store_xyzz(pfirst, t, acc);
@@ -716,7 +720,7 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
     }
   }
   __syncthreads();
-  if (owner) bucket_put<ADD>(bsum, g, xyzz_add(acc, shead[threadIdx.x + 1]));
+  if (owner) store_xyzz(bsum, g, xyzz_add(acc, shead[threadIdx.x + 1]));
 }
 
 // Queued crossing buckets (see k_accumulate): pieces pfirst/plast joined serially when the bucket
@@ -732,7 +736,6 @@ __device__ __forceinline__ G1Xyzz fixup_head(const G1Xyzz* __restrict__ pfirst, 
 // heavy queue (one bucket per block: strided partial sums of the per-thread pieces + LDS tree).
 // The two queues hold disjoint buckets (k_accumulate puts a bucket of more than kFixSerial + 1
 // pieces in both; the multi walk skips it).
-template <bool ADD>
 __global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ gst, uint32_t K,
                                                   const G1Xyzz* __restrict__ pfirst,
                                                   const G1Xyzz* __restrict__ plast,
@@ -752,7 +755,7 @@ __global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ g
       if (t1 - t0 > kFixSerial) continue;  // a heavy bucket: the other blocks' part
       G1Xyzz acc = fixup_head(pfirst, plast, s, t0, K);
       for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add_2p(acc, load_xyzz(pfirst, t));
-      bucket_put<ADD>(bsum, g, xyzz_canon2p(acc));
+      store_xyzz(bsum, g, xyzz_canon2p(acc));
     }
     return;
   }
@@ -770,7 +773,7 @@ __global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ g
       __syncthreads();
     }
     if (tid == 0) {
-      bucket_put<ADD>(bsum, g, xyzz_add(fixup_head(pfirst, plast, s, t0, K), sh[0]));
+      store_xyzz(bsum, g, xyzz_add(fixup_head(pfirst, plast, s, t0, K), sh[0]));
     }
     __syncthreads();
   }
@@ -929,6 +932,17 @@ static uint32_t plan_K(uint64_t entries, uint32_t nbt) {
   if (const char* e = getenv("SVGPU_ACC_K")) K = (uint64_t)atoi(e);
   if (K < 1) K = 1;
   return (uint32_t)K;
+}
+
+// Host-fed pieces (a fraction of the points over the whole bucket set, so few entries per bucket):
+// chunks of about two average buckets halve the crossing buckets k_fixup joins, for a few percent
+// of accumulate occupancy (device-resident sweep at 2^17 points, c = 16: K = 8 0.213 + 0.061 ms
+// fixup, K = 16 0.215 + 0.036)
+static uint32_t piece_K(uint64_t entries, uint32_t nbt) {
+  const uint32_t K = plan_K(entries, nbt);
+  if (getenv("SVGPU_ACC_K")) return K;
+  const uint64_t two_avg = 2 * (entries / nbt);
+  return (uint32_t)std::max<uint64_t>(K, std::min<uint64_t>(std::max<uint64_t>(two_avg, 16), 256));
 }
 
 MsmPlan msm_plan(size_t n) {
@@ -1111,8 +1125,8 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
 }
 
 // Bucket accumulation of a sorted piece + its crossing-bucket fixups into bsum, on stream st
-// (add_into: the piece's bucket sums are added to what bsum holds; otherwise complete buckets are
-// stored and empty ones left untouched).
+// (add_into: the piece's bucket sums are added to what bsum holds -- k_accumulate<true> starts each
+// bucket's owner segment from it; otherwise complete buckets are stored and empty ones left alone).
 static int msm_acc(const MsmPlan& p, const MsmScratch& w, const SortOut& so, const G1Aff* bases, int add_into,
                    hipStream_t st, G1Xyzz* bsum, const uint4* phix, uint32_t nsplit, hipEvent_t ev_acc_done,
                    hipEvent_t ev_fix_mid) {
@@ -1127,12 +1141,8 @@ static int msm_acc(const MsmPlan& p, const MsmScratch& w, const SortOut& so, con
   SV_HIP(hipGetLastError());
   if (ev_acc_done) SV_HIP(hipEventRecord(ev_acc_done, st));
   const uint32_t gm = std::min<uint32_t>(cdiv(p.nbt, kBlock), 1024);
-  if (add_into)
-    hipLaunchKernelGGL(k_fixup<true>, dim3(gm + 256), dim3(kBlock), 0, st, so.gst, so.K, w.pfirst, w.plast, w.multi,
-                       w.nmulti, w.heavy, w.nheavy, gm, bsum);
-  else
-    hipLaunchKernelGGL(k_fixup<false>, dim3(gm + 256), dim3(kBlock), 0, st, so.gst, so.K, w.pfirst, w.plast, w.multi,
-                       w.nmulti, w.heavy, w.nheavy, gm, bsum);
+  hipLaunchKernelGGL(k_fixup, dim3(gm + 256), dim3(kBlock), 0, st, so.gst, so.K, w.pfirst, w.plast, w.multi,
+                     w.nmulti, w.heavy, w.nheavy, gm, bsum);
   SV_HIP(hipGetLastError());
   if (ev_fix_mid) SV_HIP(hipEventRecord(ev_fix_mid, st));
   return SV_OK;
@@ -1213,7 +1223,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   for (int k = 0; k < pieces; k++) {
     const uint64_t e = (uint64_t)(pb[k + 1] - pb[k]) * ep;
     max_piece = std::max(max_piece, pb[k + 1] - pb[k]);
-    so[k].K = feed ? plan_K(e, p.nbt) : p.K;  // each piece's chunk length for its own size
+    so[k].K = feed ? piece_K(e, p.nbt) : p.K;  // each piece's chunk length for its own size
     so[k].T = cdiv(e, so[k].K);
     tst_total += (uint64_t)so[k].T + 1;
     Tmax = std::max(Tmax, so[k].T);
@@ -1347,6 +1357,48 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
     SV_HIP(hipEventRecord(ev[6], st));
     SV_HIP(hipStreamWaitEvent(cs, ev[6], 0));
     SV_HIP(hipStreamWaitEvent(ss, ev[6], 0));
+    // A feeder (the workspace's helper thread) stages the pieces back to back (a pageable copy blocks
+    // the thread that issues it: queueing each piece's ~12 launches from that same thread left the
+    // copy engine idle ~30 us per burst, rocprof trace); this thread queues a piece's sort /
+    // accumulate as soon as the feeder has recorded the piece's events.  staged = stages done (2k + 1: piece k's scalars, 2k + 2: its
+    // bases), -1 once the feeder failed.
+    std::atomic<int> staged{0}, stop{0};
+    int feed_rc = SV_OK;
+    std::string feed_err;
+    SV_TRY(ws->run_helper([&] {
+      int rc = SV_OK;
+      for (int k = 0; k < pieces && !stop.load(std::memory_order_relaxed); k++) {
+        const size_t lo = pb[k], hi = pb[k + 1];
+        rc = feed->stage_scalars(lo, hi, const_cast<Fr*>(scalars) + lo, cs, ev[8 + 3 * k]);
+        if (rc != SV_OK) break;
+        staged.store(2 * k + 1, std::memory_order_release);
+        rc = feed->stage_bases(lo, hi, const_cast<G1Aff*>(bases) + lo, cs, ev[9 + 3 * k]);
+        if (rc != SV_OK) break;
+        staged.store(2 * k + 2, std::memory_order_release);
+      }
+      if (rc != SV_OK) {
+        feed_rc = rc;
+        feed_err = sv::last_error();
+        staged.store(-1, std::memory_order_release);
+      }
+    }));
+    struct Join {  // on every exit: stop the feeder after its current stage, then wait for it
+      Workspace* ws;
+      std::atomic<int>& stop;
+      ~Join() {
+        stop.store(1);
+        ws->wait_helper();
+      }
+    } join{ws, stop};
+    auto wait_stage = [&](int v) -> int {
+      int x;
+      while ((x = staged.load(std::memory_order_acquire)) >= 0 && x < v) std::this_thread::yield();
+      if (x < 0) {
+        set_error("%s", feed_err.c_str());
+        return feed_rc;
+      }
+      return SV_OK;
+    };
     for (int k = 0; k < pieces; k++) {
       const size_t lo = pb[k], hi = pb[k + 1], m = hi - lo;
       hipEvent_t sc_ready = ev[8 + 3 * k], b_ready = ev[9 + 3 * k], sorted = ev[10 + 3 * k];
@@ -1355,11 +1407,11 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
       // GLV: piece-local virtual points (i, m + i) over the piece's bases and its slice of the table
       const uint32_t nsplit = p.glv ? (uint32_t)m : ~0u;
       uint4* phix_k = p.glv ? phix + (size_t)(p.phi64 ? 4 : 2) * lo : nullptr;
-      SV_TRY(feed->stage_scalars(lo, hi, dsc, cs, sc_ready));
+      SV_TRY(wait_stage(2 * k + 1));
       SV_HIP(hipStreamWaitEvent(ss, sc_ready, 0));
       SV_TRY(msm_sort(p, w, so[k], nullptr, dsc, m, mont_in, device, ss, nullptr, nsplit, 0, nullptr));
       SV_HIP(hipEventRecord(sorted, ss));
-      SV_TRY(feed->stage_bases(lo, hi, db, cs, b_ready));
+      SV_TRY(wait_stage(2 * k + 2));
       SV_HIP(hipStreamWaitEvent(st, b_ready, 0));
       const G1Aff* pbases = conv ? bases_m + lo : db;
       if (conv)  // canonical bases converted (and checked) once they have landed

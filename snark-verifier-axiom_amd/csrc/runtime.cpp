@@ -2,7 +2,9 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <condition_variable>
 #include <cstdlib>
+#include <thread>
 
 namespace sv {
 
@@ -100,6 +102,53 @@ int Workspace::quiesce() {
   if (copy_stream) SV_HIP(hipStreamSynchronize(copy_stream));
   if (sort_stream) SV_HIP(hipStreamSynchronize(sort_stream));
   return SV_OK;
+}
+
+struct Workspace::Helper {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::function<void()> job;
+  bool pending = false, busy = false;
+};
+
+int Workspace::run_helper(std::function<void()> job) {
+  if (!helper) {
+    helper = new Helper();
+    Helper* h = helper;
+    const int dev = device;
+    std::thread([h, dev] {
+      (void)hipSetDevice(dev);
+      for (;;) {
+        std::function<void()> j;
+        {
+          std::unique_lock<std::mutex> lk(h->mu);
+          h->cv.wait(lk, [h] { return h->pending; });
+          j = std::move(h->job);
+          h->pending = false;
+        }
+        j();
+        {
+          std::lock_guard<std::mutex> lk(h->mu);
+          h->busy = false;
+        }
+        h->cv.notify_all();
+      }
+    }).detach();  // lives with the pooled workspace, for the process
+  }
+  {
+    std::lock_guard<std::mutex> lk(helper->mu);
+    helper->job = std::move(job);
+    helper->pending = true;
+    helper->busy = true;
+  }
+  helper->cv.notify_all();
+  return SV_OK;
+}
+
+void Workspace::wait_helper() {
+  if (!helper) return;
+  std::unique_lock<std::mutex> lk(helper->mu);
+  helper->cv.wait(lk, [this] { return !helper->busy; });
 }
 
 int Workspace::ensure_sort_stream() {

@@ -55,7 +55,14 @@ struct Workspace {
   int reserve_stage(size_t bytes);   // grow-only pinned gather staging
   int ensure_copy_stream();
   int ensure_sort_stream();
-  int quiesce();  // wait for the compute and copy streams (before freeing or reusing staging)
+  int quiesce();
+  // A persistent helper thread of this workspace (created on first use, current device set once):
+  // run_helper queues `job` on it, wait_helper blocks until that job has returned.  The host-fed
+  // MSM's feeder runs here (a new std::thread per call, with its first HIP call, cost ~0.2 ms).
+  int run_helper(std::function<void()> job);
+  void wait_helper();
+  struct Helper;
+  Helper* helper = nullptr;  // wait for the compute and copy streams (before freeing or reusing staging)
 };
 
 // RAII lease of a per-device workspace; stream override optional.

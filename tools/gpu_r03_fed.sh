@@ -12,4 +12,5 @@ run() {  # name timeout cmd...
 run pytest_fed 400 python3 -u -m pytest tests/test_gpu_host_path.py tests/test_gpu_msm.py -x -q --timeout 120 --timeout-method thread
 run host_api 300 python3 tools/host_api_bench.py 20 ${FED_SPECS}
 run prof/hosttrace 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/prof/hosttrace -o run -- python3 tools/host_path_trace.py
+python3 tools/trace_timeline.py gpurun_out/prof/hosttrace -5 > gpurun_out/tl_arrays.txt; python3 tools/trace_timeline.py gpurun_out/prof/hosttrace -1 > gpurun_out/tl_refs.txt
 cat gpurun_out/host_api.log

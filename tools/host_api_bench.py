@@ -41,6 +41,9 @@ specs = sys.argv[2:] or ["", "SVGPU_H2D_PIECES=1", "SVGPU_H2D_PIECES=2", "SVGPU_
                          "SVGPU_H2D_PIECES=6", "SVGPU_H2D_PIECES=8", "SVGPU_H2D_SPLIT=1,1,2,3,3,3,3",
                          "SVGPU_H2D_SPLIT=1,2,3,3,3,2", "SVGPU_H2D_SPLIT=2,3,3,3,3,2",
                          "SVGPU_H2D_SPLIT=1,2,2,3,3,3,2"]
+rng = np.random.default_rng(1)
+perm = rng.permutation(n)
+rf_shuf = svgpu.make_refs(S.ctypes.data + 32 * perm.astype(np.uint64), B.ctypes.data + 64 * perm.astype(np.uint64))
 for spec in specs:
     for k in ("SVGPU_H2D_PIECES", "SVGPU_H2D_SPLIT", "SVGPU_GLV"):
         os.environ.pop(k, None)
@@ -48,7 +51,9 @@ for spec in specs:
         k, v = kv.split("=")
         os.environ[k] = v
     ms, r = t(lambda: svgpu.msm_arrays(B, S, M))
-    print(f"host [{spec or 'default'}]  {ms:7.3f} ms  x{ms / dms:.2f}  ok={r == ref}", flush=True)
+    rms, rr = t(lambda: svgpu.msm_refs(rf_shuf, M))
+    print(f"host [{spec or 'default'}]  {ms:7.3f} ms  x{ms / dms:.2f}  ok={r == ref}   refs {rms:7.3f} ms  "
+          f"x{rms / dms:.2f}  ok={rr == ref}", flush=True)
 for k in ("SVGPU_H2D_PIECES", "SVGPU_H2D_SPLIT", "SVGPU_GLV"):
     os.environ.pop(k, None)
 rng = np.random.default_rng(1)

@@ -1,4 +1,5 @@
-"""One host-buffer MSM (sv_bn254_g1_msm, 2^20, pageable Montgomery arrays) after warm-up, for a
+"""Host-buffer MSMs (sv_bn254_g1_msm on pageable Montgomery arrays, then sv_bn254_g1_msm_refs on
+shuffled references; 2^20, four calls each) for a
 rocprofv3 --kernel-trace --memory-copy-trace timeline of the piece pipeline."""
 import os
 import sys
@@ -23,3 +24,8 @@ B = Bd.cpu().numpy().view(np.uint64).copy()
 S = Sd.cpu().numpy().view(np.uint64).copy()
 for _ in range(4):
     svgpu.msm_arrays(B, S, M)
+# then the reference-shaped entry point (shuffled references: the gather is inside the call)
+perm = np.random.default_rng(1).permutation(n).astype(np.uint64)
+refs = svgpu.make_refs(S.ctypes.data + 32 * perm, B.ctypes.data + 64 * perm)
+for _ in range(4):
+    svgpu.msm_refs(refs, M)

@@ -935,14 +935,17 @@ static uint32_t plan_K(uint64_t entries, uint32_t nbt) {
 }
 
 // Host-fed pieces (a fraction of the points over the whole bucket set, so few entries per bucket):
-// chunks of about two average buckets halve the crossing buckets k_fixup joins, for a few percent
-// of accumulate occupancy (device-resident sweep at 2^17 points, c = 16: K = 8 0.213 + 0.061 ms
-// fixup, K = 16 0.215 + 0.036)
+// chunks of about two average buckets while that stays <= 32 entries (fewer crossing buckets for
+// k_fixup), else max(32, one average bucket); a multiple of 8.  Measured device-resident at the
+// 2^20 plan's window (c = 16, GLV), best accumulate + fixup: 2^16 points K = 8 (average bucket 4),
+// 2^17 16 (8), 3 * 2^16 24 (12), 2^18 32 (16), 349525 24-32 (21; K = 21 and 42: +8-20 %), 2^19
+// 32 (32), 2^20 64 (64) -- tools/gpu_r03_pieceK.sh.
 static uint32_t piece_K(uint64_t entries, uint32_t nbt) {
-  const uint32_t K = plan_K(entries, nbt);
-  if (getenv("SVGPU_ACC_K")) return K;
-  const uint64_t two_avg = 2 * (entries / nbt);
-  return (uint32_t)std::max<uint64_t>(K, std::min<uint64_t>(std::max<uint64_t>(two_avg, 16), 256));
+  if (getenv("SVGPU_ACC_K")) return plan_K(entries, nbt);
+  const uint64_t avg = entries / nbt;
+  uint64_t K = 2 * avg <= 32 ? 2 * avg : std::max<uint64_t>(32, avg);
+  K = std::min<uint64_t>(std::max<uint64_t>((K + 7) / 8 * 8, 8), 256);
+  return (uint32_t)K;
 }
 
 MsmPlan msm_plan(size_t n) {
@@ -1149,11 +1152,14 @@ static int msm_acc(const MsmPlan& p, const MsmScratch& w, const SortOut& so, con
 }
 
 // Host-fed piece boundaries: SVGPU_H2D_SPLIT = comma-separated weights, else `pieces` equal pieces
-// (SVGPU_H2D_PIECES), else the default schedule.  The host-fed MSM is transfer-bound (96 B per point
-// at ~54 GB/s) and a piece's accumulate runs only once its bases have landed, so the schedule starts
-// with small pieces (the accumulate starts early) and ends with a small one (little work left after
-// the last byte lands); in between, pieces are large enough to keep each accumulate efficient.
-static std::vector<size_t> piece_bounds(size_t n, int pieces) {
+// (SVGPU_H2D_PIECES), else the default schedule: 4 equal pieces from 2^18 points.  A piece's
+// accumulate runs once its bases have landed (96 B per point at ~52 GB/s), and once the first piece
+// is in, the compute stream is the bottleneck (a piece's accumulate + fixup outlasts the next
+// piece's transfer), so what counts is the total accumulate work -- smaller pieces are less efficient
+// -- against starting early and leaving little after the last byte.  Measured at 2^20 (3 boxes,
+// tools/host_api_bench.py): 4 equal pieces 2.73-2.92 ms, 2,2,3,3,3,3 2.74-3.06, 2,3,3,3,3,2
+// 2.74-3.09, 3 pieces 3.41-3.47, 6 3.17-4.20 (before per-piece K), 1 piece 3.76-3.95.
+static std::vector<size_t> piece_bounds(size_t n, int pieces, const std::vector<double>& dflt) {
   std::vector<double> wts;
   if (const char* e = getenv("SVGPU_H2D_SPLIT")) {
     for (const char* q = e; *q;) {
@@ -1168,8 +1174,10 @@ static std::vector<size_t> piece_bounds(size_t n, int pieces) {
   if (wts.empty()) {
     if (pieces > 0) {
       wts.assign(std::min(pieces, 16), 1.0);
+    } else if (n >= (size_t(1) << 18) && !dflt.empty()) {
+      wts = dflt;
     } else if (n >= (size_t(1) << 18)) {
-      wts = {2, 2, 3, 3, 3, 3};
+      wts = {1, 1, 1, 1};
     } else if (n >= (size_t(1) << 15)) {
       wts = {1, 1};
     } else {
@@ -1185,9 +1193,14 @@ static std::vector<size_t> piece_bounds(size_t n, int pieces) {
   double cum = 0;
   for (size_t k = 0; k + 1 < wts.size(); k++) {
     cum += wts[k];
-    b.push_back(std::max(b.back(), std::min(n, (size_t)((double)n * cum / tot))));
+    // boundaries on multiples of 1024 points: every piece's copies start 32-KiB aligned (5 equal
+    // pieces, boundaries 32-B aligned, measured 3.13-3.17 ms vs 2.73-2.76 for 4 and 6)
+    const size_t at = ((size_t)((double)n * cum / tot)) & ~size_t(1023);
+    b.push_back(std::max(b.back(), std::min(n, at)));
   }
   b.push_back(n);
+  b.erase(std::unique(b.begin(), b.end()), b.end());
+  if (b.size() < 2) b = {0, n};
   return b;
 }
 
@@ -1213,7 +1226,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   // host-fed inputs arrive in pieces (piece_bounds): piece k is sorted on the sort stream once its
   // scalars have landed and accumulated on the compute stream once its bases have, while later
   // pieces are still in flight
-  const std::vector<size_t> pb = feed ? piece_bounds(n, feed->pieces) : std::vector<size_t>{0, n};
+  const std::vector<size_t> pb = feed ? piece_bounds(n, feed->pieces, feed->split) : std::vector<size_t>{0, n};
   const int pieces = (int)pb.size() - 1;
   const uint32_t ep = p.glv ? 2 * p.W : p.W;  // entries per real point
   size_t max_piece = 0;
@@ -1424,9 +1437,13 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
                            p.phi64, conv ? nullptr : w.err);
       SV_HIP(hipGetLastError());
       SV_HIP(hipStreamWaitEvent(st, sorted, 0));
-      if (k > 0) SV_HIP(hipMemsetAsync(w.err + 1, 0, 8, st));  // fixup queue counters
       if (k == 0) SV_HIP(hipEventRecord(ev[2], st));
-      SV_TRY(msm_acc(p, w, so[k], pbases, k > 0 ? 1 : 0, st, bsum, phix_k, nsplit,
+      // each piece has its own fixup queue counters (err[1 + 2k], err[2 + 2k], zeroed with the
+      // error flag), so no per-piece memset sits between the accumulates
+      MsmScratch wk = w;
+      wk.nheavy = w.err + 1 + 2 * k;
+      wk.nmulti = w.err + 2 + 2 * k;
+      SV_TRY(msm_acc(p, wk, so[k], pbases, k > 0 ? 1 : 0, st, bsum, phix_k, nsplit,
                      k == pieces - 1 ? ev[3] : nullptr, nullptr));
     }
   }

@@ -5,6 +5,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <functional>
+#include <vector>
 
 #include "../../include/svgpu.h"
 #include "host_ec.hpp"
@@ -40,7 +41,9 @@ int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int for
 // with the piece's sort enqueued in between: pageable transfers block the calling thread, so the
 // sort then runs while the bases are still in flight.
 struct MsmFeed {
-  int pieces = 4;
+  int pieces = 0;             // equal pieces (0: split, else the default schedule)
+  std::vector<double> split;  // piece weights from 2^18 points when SVGPU_H2D_* are unset
+
   std::function<int(size_t lo, size_t hi, void* d_scalars, hipStream_t copy_stream, hipEvent_t ready)> stage_scalars;
   std::function<int(size_t lo, size_t hi, void* d_bases, hipStream_t copy_stream, hipEvent_t ready)> stage_bases;
 };

@@ -8,8 +8,9 @@ from svgpu import device as dv
 from oracle import bn254 as ob
 svgpu.init()
 dev = torch.device("cuda:0")
-log_n = int(sys.argv[1])
-n = 1 << log_n
+arg = sys.argv[1]  # LOG_N, or n=COUNT for an arbitrary size
+n = int(arg[2:]) if arg.startswith("n=") else 1 << int(arg)
+log_n = arg
 B = dv.gen_bases(dv.empty_bases(n, dev), ob.SEED_BASES, 0)
 S = dv.gen_scalars(dv.empty_scalars(n, dev), ob.SEED_SCALARS, 0)
 torch.cuda.synchronize()

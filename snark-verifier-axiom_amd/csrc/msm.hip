@@ -43,6 +43,7 @@
 #include "glv.hpp"
 #include "host_ec.hpp"
 #include "msm.hpp"
+#include "quad.hpp"
 #include "runtime.hpp"
 
 namespace sv {
@@ -723,6 +724,20 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
   if (owner) store_xyzz(bsum, g, xyzz_add(acc, shead[threadIdx.x + 1]));
 }
 
+// one coordinate (c = 0..3: X, Y, ZZ, ZZZ) of an XYZZ value, for the quad-form kernels (quad.hpp)
+__device__ __forceinline__ Fq ld_coord(const G1Xyzz* p, int c) {
+  const uint4* q = reinterpret_cast<const uint4*>(p) + 2 * c;
+  const uint4 x = q[0], y = q[1];
+  Fq r;
+  r.v[0] = x.x; r.v[1] = x.y; r.v[2] = x.z; r.v[3] = x.w;
+  r.v[4] = y.x; r.v[5] = y.y; r.v[6] = y.z; r.v[7] = y.w;
+  return r;
+}
+__device__ __forceinline__ void st_coord(G1Xyzz* p, int c, const Fq& v) {
+  uint4* q = reinterpret_cast<uint4*>(p) + 2 * c;
+  q[0] = make_uint4(v.v[0], v.v[1], v.v[2], v.v[3]);
+  q[1] = make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]);
+}
 // Queued crossing buckets (see k_accumulate): pieces pfirst/plast joined serially when the bucket
 // spans at most kFixSerial + 1 threads; longer ones (skewed digits: all-equal scalars, a short top
 // window) are queued by k_accumulate for k_fixup's heavy blocks instead of being walked serially.
@@ -747,15 +762,19 @@ __global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ g
   __shared__ G1Xyzz sh[kBlock];
   const uint32_t tid = threadIdx.x;
   if (blockIdx.x < gm) {  // block-uniform
+    // one bucket per QUAD of lanes (quad.hpp: lane c = coordinate c): the chain of at most
+    // kFixSerial additions is latency-bound (a few waves per SIMD), so 4-level quad additions
+    // shorten it 2-3x; every branch below is uniform within the quad
     const uint32_t nm = *nmulti;
-    for (uint32_t h = blockIdx.x * blockDim.x + tid; h < nm; h += gm * blockDim.x) {
+    const int c = tid & 3;
+    for (uint32_t h = (blockIdx.x * blockDim.x + tid) >> 2; h < nm; h += (gm * blockDim.x) >> 2) {
       const uint32_t g = multi[h];
       const uint32_t s = gst[g], e = gst[g + 1];
       const uint32_t t0 = s / K, t1 = (e - 1) / K;
       if (t1 - t0 > kFixSerial) continue;  // a heavy bucket: the other blocks' part
-      G1Xyzz acc = fixup_head(pfirst, plast, s, t0, K);
-      for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add_2p(acc, load_xyzz(pfirst, t));
-      store_xyzz(bsum, g, xyzz_canon2p(acc));
+      Fq acc = ld_coord(s == t0 * K ? pfirst + t0 : plast + t0, c);
+      for (uint32_t t = t0 + 1; t <= t1; t++) acc = quad::add_2p(acc, ld_coord(pfirst + t, c), c);
+      st_coord(bsum + g, c, fe_canon2p(acc));
     }
     return;
   }
@@ -904,6 +923,77 @@ __global__ void __launch_bounds__(kGroupBlock) k_group_sum(const G1Xyzz* __restr
       if (k != pp) s = xyzz_add_2p(s, load_xyzz(part, gid * P + k));
   }
   store_xyzz(out, gid, xyzz_canon2p(s));
+}
+
+// The same subset sums with every XYZZ addition split over a quad of lanes (quad.hpp: lane
+// c = lane & 3 holds coordinate c; 4 product levels per addition instead of ~14 dependent products):
+// the tree is latency-bound (one wave per SIMD, most lanes idle in its upper levels), so a 3-4x
+// shorter addition shortens the whole kernel.  512-thread blocks: strided member sums with whole
+// per-lane additions (4 per lane: throughput work), then the tree in quad form -- a 4 x 4 transpose
+// turns each quad's four sums into quad-form points (two levels), then four in-wave levels (lane
+// shifts of 32 .. 4) and three cross-wave levels through LDS: 9 quad-addition levels instead of 9
+// whole-addition levels.
+__device__ __forceinline__ const G1Xyzz* group_member_ptr(const G1Xyzz* __restrict__ acc,
+                                                          const G1Xyzz* __restrict__ tot, uint32_t w, uint32_t g,
+                                                          uint32_t J, uint32_t H, uint32_t m) {
+  if (g < 2) return acc + (w * J + g * H + m);
+  const uint32_t k = g - 2;
+  const uint32_t j = ((m >> k) << (k + 1)) | (1u << k) | (m & ((1u << k) - 1));
+  return tot + (w * J + j);
+}
+__global__ void __launch_bounds__(kGroupBlock) k_group_sum_q(const G1Xyzz* __restrict__ acc,
+                                                             const G1Xyzz* __restrict__ tot, uint32_t J,
+                                                             uint32_t logJ, uint32_t P, G1Xyzz* __restrict__ out,
+                                                             G1Xyzz* __restrict__ part, uint32_t* __restrict__ cnt) {
+  constexpr int kWaves = kGroupBlock / 64;
+  __shared__ Fq sh[kWaves][4];
+  const uint32_t NG = 2 + logJ, H = J / 2;
+  const uint32_t gid = blockIdx.x / P, pp = blockIdx.x % P, w = gid / NG, g = gid % NG, tid = threadIdx.x;
+  const int c = tid & 3, lane = tid & 63, wave = tid >> 6;
+  const uint32_t m0 = (uint32_t)((uint64_t)H * pp / P), m1 = (uint32_t)((uint64_t)H * (pp + 1) / P);
+  // strided member sums with whole additions per lane (throughput work: every lane busy), two loads
+  // in flight per addition pair, as k_group_sum
+  G1Xyzz ps = G1Xyzz::identity();
+  uint32_t m = m0 + tid;
+  for (; m + kGroupBlock < m1; m += 2 * kGroupBlock) {
+    const G1Xyzz x0 = group_member(acc, tot, w, g, J, H, m);
+    const G1Xyzz x1 = group_member(acc, tot, w, g, J, H, m + kGroupBlock);
+    ps = xyzz_add_2p(ps, x0);
+    ps = xyzz_add_2p(ps, x1);
+  }
+  if (m < m1) ps = xyzz_add_2p(ps, group_member(acc, tot, w, g, J, H, m));
+  // the tree in quad form: transpose the quad's four points to coordinates, add them (two levels),
+  // then quads across the wave and across waves
+  Fq v[4] = {ps.X, ps.Y, ps.ZZ, ps.ZZZ};
+  quad::transpose(v, c);
+  Fq s = quad::add_2p(quad::add_2p(v[0], v[1], c), quad::add_2p(v[2], v[3], c), c);
+#pragma unroll
+  for (int off = 32; off >= 4; off >>= 1) {
+    const Fq o = quad::down(s, off);
+    if (lane < off) s = quad::add_2p(s, o, c);
+  }
+  if (lane < 4) sh[wave][c] = s;
+  __syncthreads();
+  if (wave != 0) return;
+  if (lane < 4 * kWaves) s = sh[lane >> 2][c];
+#pragma unroll
+  for (int off = 2 * kWaves; off >= 4; off >>= 1) {
+    const Fq o = quad::down(s, off);
+    if (lane < off) s = quad::add_2p(s, o, c);
+  }
+  if (lane >= 4) return;
+  if (P > 1) {
+    st_coord(part + blockIdx.x, c, s);
+    __threadfence();
+    uint32_t prev = 0;
+    if (lane == 0) prev = atomicAdd(&cnt[gid], 1u);
+    prev = (uint32_t)__shfl((int)prev, 0);
+    if (prev != P - 1) return;  // uniform over the quad
+    __threadfence();
+    for (uint32_t k = 0; k < P; k++)
+      if (k != pp) s = quad::add_2p(s, ld_coord(part + gid * P + k, c), c);
+  }
+  st_coord(out + gid, c, fe_canon2p(s));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1453,8 +1543,13 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   // of these occupancy-bound kernels takes nearly as long as the whole -- reduce 0.40 -> 0.67 ms.)
   hipLaunchKernelGGL(k_wsum, dim3(cdiv((uint64_t)p.J * p.W, kBlock)), dim3(kBlock), 0, st, bsum,
                      pieces > 1 ? nullptr : so[0].gst, p.B, p.J, 1u << p.logL, p.W, 1, racc, rtot);
-  hipLaunchKernelGGL(k_group_sum, dim3(p.NG * p.W * gparts), dim3(kGroupBlock), 0, st, racc, rtot, p.J, p.logJ,
-                     gparts, ping, gpart, w.err + 64);
+  const bool group_quad = !getenv("SVGPU_GROUP_QUAD") || atoi(getenv("SVGPU_GROUP_QUAD")) != 0;
+  if (group_quad)
+    hipLaunchKernelGGL(k_group_sum_q, dim3(p.NG * p.W * gparts), dim3(kGroupBlock), 0, st, racc, rtot, p.J, p.logJ,
+                       gparts, ping, gpart, w.err + 64);
+  else
+    hipLaunchKernelGGL(k_group_sum, dim3(p.NG * p.W * gparts), dim3(kGroupBlock), 0, st, racc, rtot, p.J, p.logJ,
+                       gparts, ping, gpart, w.err + 64);
   SV_HIP(hipGetLastError());
   if (!lean) SV_HIP(hipEventRecord(ev[5], st));
   SV_HIP(hipMemcpyAsync(ws->pinned, ping, nfinal * sizeof(G1Xyzz) + 4, hipMemcpyDeviceToHost, st));

@@ -724,20 +724,6 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
   if (owner) store_xyzz(bsum, g, xyzz_add(acc, shead[threadIdx.x + 1]));
 }
 
-// one coordinate (c = 0..3: X, Y, ZZ, ZZZ) of an XYZZ value, for the quad-form kernels (quad.hpp)
-__device__ __forceinline__ Fq ld_coord(const G1Xyzz* p, int c) {
-  const uint4* q = reinterpret_cast<const uint4*>(p) + 2 * c;
-  const uint4 x = q[0], y = q[1];
-  Fq r;
-  r.v[0] = x.x; r.v[1] = x.y; r.v[2] = x.z; r.v[3] = x.w;
-  r.v[4] = y.x; r.v[5] = y.y; r.v[6] = y.z; r.v[7] = y.w;
-  return r;
-}
-__device__ __forceinline__ void st_coord(G1Xyzz* p, int c, const Fq& v) {
-  uint4* q = reinterpret_cast<uint4*>(p) + 2 * c;
-  q[0] = make_uint4(v.v[0], v.v[1], v.v[2], v.v[3]);
-  q[1] = make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]);
-}
 // Queued crossing buckets (see k_accumulate): pieces pfirst/plast joined serially when the bucket
 // spans at most kFixSerial + 1 threads; longer ones (skewed digits: all-equal scalars, a short top
 // window) are queued by k_accumulate for k_fixup's heavy blocks instead of being walked serially.
@@ -772,9 +758,9 @@ __global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ g
       const uint32_t s = gst[g], e = gst[g + 1];
       const uint32_t t0 = s / K, t1 = (e - 1) / K;
       if (t1 - t0 > kFixSerial) continue;  // a heavy bucket: the other blocks' part
-      Fq acc = ld_coord(s == t0 * K ? pfirst + t0 : plast + t0, c);
-      for (uint32_t t = t0 + 1; t <= t1; t++) acc = quad::add_2p(acc, ld_coord(pfirst + t, c), c);
-      st_coord(bsum + g, c, fe_canon2p(acc));
+      Fq acc = quad::ld(s == t0 * K ? pfirst + t0 : plast + t0, c);
+      for (uint32_t t = t0 + 1; t <= t1; t++) acc = quad::add_2p(acc, quad::ld(pfirst + t, c), c);
+      quad::st(bsum + g, c, fe_canon2p(acc));
     }
     return;
   }
@@ -933,14 +919,6 @@ __global__ void __launch_bounds__(kGroupBlock) k_group_sum(const G1Xyzz* __restr
 // turns each quad's four sums into quad-form points (two levels), then four in-wave levels (lane
 // shifts of 32 .. 4) and three cross-wave levels through LDS: 9 quad-addition levels instead of 9
 // whole-addition levels.
-__device__ __forceinline__ const G1Xyzz* group_member_ptr(const G1Xyzz* __restrict__ acc,
-                                                          const G1Xyzz* __restrict__ tot, uint32_t w, uint32_t g,
-                                                          uint32_t J, uint32_t H, uint32_t m) {
-  if (g < 2) return acc + (w * J + g * H + m);
-  const uint32_t k = g - 2;
-  const uint32_t j = ((m >> k) << (k + 1)) | (1u << k) | (m & ((1u << k) - 1));
-  return tot + (w * J + j);
-}
 __global__ void __launch_bounds__(kGroupBlock) k_group_sum_q(const G1Xyzz* __restrict__ acc,
                                                              const G1Xyzz* __restrict__ tot, uint32_t J,
                                                              uint32_t logJ, uint32_t P, G1Xyzz* __restrict__ out,
@@ -983,7 +961,7 @@ __global__ void __launch_bounds__(kGroupBlock) k_group_sum_q(const G1Xyzz* __res
   }
   if (lane >= 4) return;
   if (P > 1) {
-    st_coord(part + blockIdx.x, c, s);
+    quad::st(part + blockIdx.x, c, s);
     __threadfence();
     uint32_t prev = 0;
     if (lane == 0) prev = atomicAdd(&cnt[gid], 1u);
@@ -991,9 +969,9 @@ __global__ void __launch_bounds__(kGroupBlock) k_group_sum_q(const G1Xyzz* __res
     if (prev != P - 1) return;  // uniform over the quad
     __threadfence();
     for (uint32_t k = 0; k < P; k++)
-      if (k != pp) s = quad::add_2p(s, ld_coord(part + gid * P + k, c), c);
+      if (k != pp) s = quad::add_2p(s, quad::ld(part + gid * P + k, c), c);
   }
-  st_coord(out + gid, c, fe_canon2p(s));
+  quad::st(out + gid, c, fe_canon2p(s));
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -25,6 +25,7 @@
 #include "curve.hpp"
 #include "glv.hpp"
 #include "msm_batch.hpp"
+#include "quad.hpp"
 #include "runtime.hpp"
 
 namespace sv {
@@ -358,6 +359,38 @@ __global__ void __launch_bounds__(64) k_msm_batch_horner(const G1Xyzz* __restric
   }
 }
 
+// ---- Step 3, quad form (default): one QUAD of lanes per MSM (quad.hpp: lane c holds coordinate c),
+// 16 MSMs per wave; a doubling is 3 product levels and an addition 4, operands moved by DPP inside
+// the quad -- no LDS slots and no wave-wide syncs, and the batch runs 16 chains per wave instead
+// of one.  The lanes of a quad share every branch (quad-uniform), so DPP always reads live lanes.
+template <int C>
+__global__ void __launch_bounds__(64) k_msm_batch_horner_q(const G1Xyzz* __restrict__ Tg,
+                                                           const uint32_t* __restrict__ ids, uint32_t count,
+                                                           int mont, G1Aff* __restrict__ out) {
+  constexpr int W = BatchCfg<C>::W;
+  const int c = threadIdx.x & 3;
+  const uint32_t qi = blockIdx.x * 16 + (threadIdx.x >> 2);
+  if (qi >= count) return;  // uniform within the quad
+  const uint32_t id = ids ? ids[qi] : qi;
+  const G1Xyzz* T = Tg + (size_t)id * W;
+  Fq acc = quad::ld(T + W - 1, c);
+  for (int w = W - 2; w >= 0; w--) {
+#pragma unroll 1
+    for (int i = 0; i < C; i++) acc = quad::dbl_2p(acc, c);
+    acc = quad::add_2p(acc, quad::ld(T + w, c), c);
+  }
+  const G1Xyzz r = xyzz_canon2p(quad::gather(acc));
+  if (c != 0) return;
+  G1Aff a = xyzz_to_affine(r);
+  if (!mont && !r.is_identity()) {
+    a.x = fe_from_mont(a.x);
+    a.y = fe_from_mont(a.y);
+  }
+  uint32_t* o = reinterpret_cast<uint32_t*>(out + id);
+  st_fq(o, a.x);
+  st_fq(o + 8, a.y);
+}
+
 // ---- Precomputed fixed bases (base tables) -------------------------------------
 // A table row P is stored as its window multiples Q_w = 2^(8 w) P, w < kFixW (affine, Montgomery),
 // so sum_i k_i P_i = sum_i sum_w d_iw Q_iw: every signed 8-bit digit of every term lands in ONE set
@@ -548,14 +581,24 @@ int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t*
   const Fr* s = static_cast<const Fr*>(d_scalars);
   G1Aff* o = static_cast<G1Aff*>(d_out);
   const dim3 grid((uint32_t)count, WG);
+  // SVGPU_BATCH_QUAD=0: the one-wave-per-MSM Horner (LDS slots, 4 lanes) instead of the quad form
+  const bool quad_horner = !getenv("SVGPU_BATCH_QUAD") || atoi(getenv("SVGPU_BATCH_QUAD")) != 0;
   if (c == 5) {
     hipLaunchKernelGGL(k_msm_batch_windows<5>, grid, dim3(kThreads), 0, st, b, s, d_offsets, d_ids, mont, Tg, err,
                        d_bidx, table_len, mont_b);
-    hipLaunchKernelGGL(k_msm_batch_horner<5>, dim3((uint32_t)count), dim3(64), 0, st, Tg, d_ids, mont, o);
+    if (quad_horner)
+      hipLaunchKernelGGL(k_msm_batch_horner_q<5>, dim3((uint32_t)((count + 15) / 16)), dim3(64), 0, st, Tg, d_ids,
+                         (uint32_t)count, mont, o);
+    else
+      hipLaunchKernelGGL(k_msm_batch_horner<5>, dim3((uint32_t)count), dim3(64), 0, st, Tg, d_ids, mont, o);
   } else {
     hipLaunchKernelGGL(k_msm_batch_windows<8>, grid, dim3(kThreads), 0, st, b, s, d_offsets, d_ids, mont, Tg, err,
                        d_bidx, table_len, mont_b);
-    hipLaunchKernelGGL(k_msm_batch_horner<8>, dim3((uint32_t)count), dim3(64), 0, st, Tg, d_ids, mont, o);
+    if (quad_horner)
+      hipLaunchKernelGGL(k_msm_batch_horner_q<8>, dim3((uint32_t)((count + 15) / 16)), dim3(64), 0, st, Tg, d_ids,
+                         (uint32_t)count, mont, o);
+    else
+      hipLaunchKernelGGL(k_msm_batch_horner<8>, dim3((uint32_t)count), dim3(64), 0, st, Tg, d_ids, mont, o);
   }
   SV_HIP(hipGetLastError());
   SV_HIP(hipMemcpyAsync(ws->pinned, err, 4, hipMemcpyDeviceToHost, st));

@@ -31,7 +31,7 @@ __device__ __forceinline__ Fq pick(bool c, const Fq& a, const Fq& b) {
   return r;
 }
 
-// dbl-2008-s-1 of a (not the identity; the caller selects): 3 product levels
+// dbl-2008-s-1 of a: 3 product levels (the identity stays the identity: ZZ3 = V ZZ = 0)
 //   1: V = U^2 (U = 2Y) | X^2
 //   2: W = U V | S = X V | M^2 (M = 3 X^2) | ZZ3 = V ZZ
 //   3: M (S - X3) | W Y | ZZZ3 = W ZZZ ;  X3 = M^2 - 2S, Y3 = M (S - X3) - W Y
@@ -121,6 +121,25 @@ __device__ __forceinline__ void transpose(Fq v[4], int c) {
     v[2] = pick(b0, r2, v[2]);
     v[3] = pick(b0, v[3], r2);
   }
+}
+
+// coordinate c (0..3: X, Y, ZZ, ZZZ) of an XYZZ value in memory
+__device__ __forceinline__ Fq ld(const G1Xyzz* p, int c) {
+  const uint4* q = reinterpret_cast<const uint4*>(p) + 2 * c;
+  const uint4 x = q[0], y = q[1];
+  Fq r;
+  r.v[0] = x.x; r.v[1] = x.y; r.v[2] = x.z; r.v[3] = x.w;
+  r.v[4] = y.x; r.v[5] = y.y; r.v[6] = y.z; r.v[7] = y.w;
+  return r;
+}
+__device__ __forceinline__ void st(G1Xyzz* p, int c, const Fq& v) {
+  uint4* q = reinterpret_cast<uint4*>(p) + 2 * c;
+  q[0] = make_uint4(v.v[0], v.v[1], v.v[2], v.v[3]);
+  q[1] = make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]);
+}
+// the whole point on every lane of the quad
+__device__ __forceinline__ G1Xyzz gather(const Fq& a) {
+  return {perm<qp(0, 0, 0, 0)>(a), perm<qp(1, 1, 1, 1)>(a), perm<qp(2, 2, 2, 2)>(a), perm<qp(3, 3, 3, 3)>(a)};
 }
 
 // lane + `lanes` (a multiple of 4) of the same coordinate, across the wave

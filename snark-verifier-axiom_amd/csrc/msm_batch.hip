@@ -220,7 +220,193 @@ __global__ void __launch_bounds__(kThreads) k_msm_batch_windows(const G1Aff* __r
     }
     __syncthreads();
   }
-  if (tid < nw) Tg[(size_t)id * W + w0 + tid] = T[tid];
+  if (tid < nw) Tg[(size_t)blockIdx.x * W + w0 + tid] = T[tid];  // by batch position (ids may skip MSMs)
+}
+
+// ---- Steps 1 + 2, quad form (default for c = 5, i.e. MSMs of <= 256 terms) ----------------------
+// k_batch_prep: one thread per term, once: scalar checks + GLV split + the signed digits of every
+// window of both halves (u8: magnitude | sign << 7, laid out [msm][window][half-term] so a window's
+// wave reads them contiguously), and the term's two points P and phi(P) = (beta x, y) in Montgomery
+// form (bases checked / converted / looked up in the table here, identity (0, 0) kept).
+// k_batch_windows_q: one wave per (MSM, window): an LDS counting sort of the window's digits into its
+// B = 16 buckets, then ONE QUAD of lanes per bucket summing its entries with quad-form mixed adds
+// (quad.hpp), then sum_b (b + 1) S_b = sum_b R_b over the suffix sums R_b = sum_{b' >= b} S_b': a
+// 4-level scan and a 4-level tree across the wave's 16 quads.  The old kernel ran ~20 dependent
+// whole additions per window on one wave per SIMD (a per-lane bucket chain, a divergent weighting
+// double-and-add, a shuffle tree); here every level is one quad operation.
+constexpr int kQC = 5;                       // window bits of the quad path
+constexpr int kQB = 1 << (kQC - 1);          // 16 buckets: one quad each in a 64-lane wave
+constexpr int kQW = BatchCfg<kQC>::W;        // 26 windows of a 128-bit GLV half
+constexpr int kQMaxTerms = 256;              // half-terms of one window sorted in LDS at once
+
+__global__ void __launch_bounds__(kThreads) k_batch_prep(const G1Aff* __restrict__ bases,
+                                                         const Fr* __restrict__ scalars,
+                                                         const uint64_t* __restrict__ off,
+                                                         const uint32_t* __restrict__ ids, int mont,
+                                                         uint32_t max_terms, uint8_t* __restrict__ dig,
+                                                         G1Aff* __restrict__ pts, uint32_t* __restrict__ err,
+                                                         const uint32_t* __restrict__ bidx, uint64_t tlen,
+                                                         int mont_b) {
+  const uint32_t k = blockIdx.x;  // position in the batch
+  const uint32_t id = ids ? ids[k] : k;
+  const uint64_t b0 = off[id], e0 = off[id + 1];
+  const uint32_t i = blockIdx.y * kThreads + threadIdx.x;  // term of this MSM
+  if (b0 + i >= e0) return;
+  const uint64_t t = b0 + i;
+  Fr s;
+  {
+    const Fq q = ld_fq(reinterpret_cast<const uint32_t*>(scalars + t));
+#pragma unroll
+    for (int j = 0; j < 8; j++) s.v[j] = q.v[j];
+  }
+  if (!s.is_reduced()) atomicOr(err, 2u);
+  if (mont) s = fe_from_mont(s);
+  uint64_t bi = t;
+  if (bidx) {
+    const uint32_t ti = bidx[t];
+    if (ti >= tlen) {
+      atomicOr(err, 4u);
+      s = Fr::zero();
+      bi = 0;
+    } else {
+      bi = ti;
+    }
+  }
+  uint32_t hv[2][4];
+  glv_split(s.v, hv[0], hv[1]);
+  const size_t HM = 2 * (size_t)max_terms;  // half-terms per (msm, window) row
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint32_t sg = hv[h][3] >> 31;
+    hv[h][3] &= 0x7fffffffu;
+    uint32_t carry = 0;
+    for (int w = 0; w < kQW; w++) {
+      const int pos = w * kQC, limb = pos >> 5, sh = pos & 31;
+      const uint32_t lo = limb < 4 ? hv[h][limb] : 0u;
+      const uint32_t hi = limb + 1 < 4 ? hv[h][limb + 1] : 0u;
+      uint32_t bits = sh ? ((lo >> sh) | (hi << (32 - sh))) : lo;
+      bits = (bits & ((1u << kQC) - 1)) + carry;
+      uint32_t mag, neg;
+      if (bits > (uint32_t)kQB) {  // digit bits - 2^C < 0 (bits == 2^C: digit 0, carry 1)
+        mag = (1u << kQC) - bits;
+        neg = mag ? 1u : 0u;
+        carry = 1;
+      } else {
+        mag = bits;
+        neg = 0;
+        carry = 0;
+      }
+      dig[((size_t)k * kQW + w) * HM + 2 * i + h] = (uint8_t)(mag | ((neg ^ sg) << 7));
+    }
+  }
+  const uint32_t* bp = reinterpret_cast<const uint32_t*>(bases + bi);
+  Fq x = ld_fq(bp), y = ld_fq(bp + 8);
+  if (!x.is_reduced() || !y.is_reduced()) {  // same contract as the single-MSM path
+    atomicOr(err, 1u);
+    x = y = Fq::zero();
+  }
+  const bool ident = x.is_zero() && y.is_zero();
+  if (!mont_b && !ident) {
+    x = fe_to_mont(x);
+    y = fe_to_mont(y);
+  }
+  uint32_t* o = reinterpret_cast<uint32_t*>(pts + 2 * ((size_t)k * max_terms + i));
+  st_fq(o, x);
+  st_fq(o + 8, y);
+  st_fq(o + 16, x * fq_const(GLV_BETA_MONT));  // phi(P); the identity maps to itself
+  st_fq(o + 24, y);
+}
+
+// acc (quad form, 2p domain) + the affine point (x2, y2) (reduced, not the identity): madd-2008-s
+// in 4 levels -- U2 = x2 ZZ1 | S2 = y2 ZZZ1, then PP = P^2 | RR = R^2, then PPP | Q = X1 PP |
+// ZZ3 = ZZ1 PP, then R (Q - X3) | Y1 PPP | ZZZ3 = ZZZ1 PPP
+__device__ __forceinline__ Fq quad_madd_2p(const Fq& a, const Fq& x2, const Fq& y2, int c) {
+  using namespace quad;
+  const Fq zz = perm<qp(2, 2, 2, 2)>(a), zzz = perm<qp(3, 3, 3, 3)>(a);
+  const Fq X1 = perm<qp(0, 0, 0, 0)>(a), Y1 = perm<qp(1, 1, 1, 1)>(a);
+  const Fq L1 = fe_mul_lazy(c == 0 ? x2 : y2, c == 0 ? zz : zzz);  // q0 U2, q1 S2 (q2, q3 repeat q1)
+  const Fq d = fe_sub2p(perm<qp(0, 1, 1, 1)>(L1), pick(c == 0, X1, Y1));  // q0 P, q1..3 R
+  const Fq L2 = fe_mul_lazy(d, d);                                       // q0 PP, q1 RR
+  const Fq PP = perm<qp(0, 0, 0, 0)>(L2), P = perm<qp(0, 0, 0, 0)>(d);
+  const Fq L3 = fe_mul_lazy(c == 0 ? P : (c == 1 ? X1 : zz), PP);        // q0 PPP, q1 Q, q2 ZZ3
+  const Fq PPP = perm<qp(0, 0, 0, 0)>(L3), Q = perm<qp(1, 1, 1, 1)>(L3);
+  const Fq X3 = fe_sub2p(fe_sub2p(fe_sub2p(perm<qp(1, 1, 1, 1)>(L2), PPP), Q), Q);
+  const Fq R = perm<qp(1, 1, 1, 1)>(d);
+  const Fq L4 = fe_mul_lazy(c == 0 ? R : (c == 1 ? Y1 : zzz), c == 0 ? fe_sub2p(Q, X3) : PPP);
+  const Fq Y3 = fe_sub2p(perm<qp(0, 0, 0, 0)>(L4), perm<qp(1, 1, 1, 1)>(L4));
+  // the lane moves run on every lane of the quad BEFORE the per-lane choice: a DPP move inside a
+  // ?: branch executes with the other lanes masked off and reads a dead source lane
+  const Fq ZZ3 = perm<qp(2, 2, 2, 2)>(L3), ZZZ3 = perm<qp(2, 2, 2, 2)>(L4);
+  Fq r = c == 0 ? X3 : (c == 1 ? Y3 : (c == 2 ? ZZ3 : ZZZ3));
+  const bool a_id = zz.is_zero();
+  const bool p0 = fe_is_zero2p(P), r0 = fe_is_zero2p(R);
+  const bool same = !a_id && p0 && r0;
+  if (__builtin_expect(__any(same), 0)) {
+    const Fq t = dbl_2p(a, c);
+    if (same) r = t;
+  }
+  if (!a_id && p0 && !r0) r = Fq::zero();
+  if (a_id) r = c == 0 ? x2 : (c == 1 ? y2 : Fq::one());  // (x2, y2, 1, 1)
+  return r;
+}
+
+__global__ void __launch_bounds__(64) k_batch_windows_q(const uint64_t* __restrict__ off,
+                                                        const uint32_t* __restrict__ ids, uint32_t max_terms,
+                                                        const uint8_t* __restrict__ dig,
+                                                        const G1Aff* __restrict__ pts, G1Xyzz* __restrict__ Tg) {
+  __shared__ uint32_t cnt[kQB], start[kQB + 1];
+  __shared__ uint16_t lst[2 * kQMaxTerms];
+  const uint32_t k = blockIdx.x, w = blockIdx.y, lane = threadIdx.x;
+  const uint32_t id = ids ? ids[k] : k;
+  const uint32_t m = (uint32_t)(off[id + 1] - off[id]);
+  const uint8_t* dg = dig + ((size_t)k * kQW + w) * 2 * (size_t)max_terms;
+  if (lane < kQB) cnt[lane] = 0;
+  __syncthreads();
+  for (uint32_t j = lane; j < 2 * m; j += 64) {
+    const uint32_t d = dg[j];
+    if (d & 0x7f) atomicAdd(&cnt[(d & 0x7f) - 1], 1u);
+  }
+  __syncthreads();
+  if (lane == 0) {
+    uint32_t a = 0;
+    for (int b = 0; b < kQB; b++) {
+      start[b] = a;
+      a += cnt[b];
+      cnt[b] = start[b];
+    }
+    start[kQB] = a;
+  }
+  __syncthreads();
+  for (uint32_t j = lane; j < 2 * m; j += 64) {
+    const uint32_t d = dg[j];
+    if (d & 0x7f) lst[atomicAdd(&cnt[(d & 0x7f) - 1], 1u)] = (uint16_t)(j | ((d >> 7) << 15));
+  }
+  __syncthreads();
+  // quad b sums bucket b (digit magnitude b + 1); every branch is uniform within the quad
+  const int c = lane & 3, b = lane >> 2;
+  const G1Aff* pk = pts + 2 * (size_t)k * max_terms;
+  Fq S = Fq::zero();
+  for (uint32_t e = start[b]; e < start[b + 1]; e++) {
+    const uint32_t v = lst[e];
+    const uint32_t* pp = reinterpret_cast<const uint32_t*>(pk + (v & 0x7fff));
+    const Fq x = ld_fq(pp);
+    Fq y = ld_fq(pp + 8);
+    if (x.is_zero() && y.is_zero()) continue;  // identity base
+    if (v >> 15) y = -y;
+    S = quad_madd_2p(S, x, y, c);
+  }
+  // suffix sums R_b = sum_{b' >= b} S_b' (Hillis-Steele over the quads), then sum_b R_b
+#pragma unroll
+  for (int dq = 1; dq < kQB; dq <<= 1) {
+    const Fq o = quad::down(S, 4 * dq);
+    if (b + dq < kQB) S = quad::add_2p(S, o, c);
+  }
+#pragma unroll
+  for (int dq = kQB / 2; dq >= 1; dq >>= 1) {
+    const Fq o = quad::down(S, 4 * dq);
+    if (b < dq) S = quad::add_2p(S, o, c);
+  }
+  if (b == 0) quad::st(Tg + (size_t)k * kQW + w, c, fe_canon2p(S));
 }
 
 // ---- Step 3: Horner over the window sums with the independent products of each XYZZ doubling /
@@ -331,7 +517,7 @@ __global__ void __launch_bounds__(64) k_msm_batch_horner(const G1Xyzz* __restric
   __shared__ Fq R[kSlots];
   const int lane = threadIdx.x;
   const uint32_t id = ids ? ids[blockIdx.x] : blockIdx.x;
-  const G1Xyzz* T = Tg + (size_t)id * W;
+  const G1Xyzz* T = Tg + (size_t)blockIdx.x * W;
   if (lane == 0) {
     const G1Xyzz t = T[W - 1];
     R[sX] = t.X, R[sY] = t.Y, R[sZZ] = t.ZZ, R[sZZZ] = t.ZZZ;
@@ -372,7 +558,7 @@ __global__ void __launch_bounds__(64) k_msm_batch_horner_q(const G1Xyzz* __restr
   const uint32_t qi = blockIdx.x * 16 + (threadIdx.x >> 2);
   if (qi >= count) return;  // uniform within the quad
   const uint32_t id = ids ? ids[qi] : qi;
-  const G1Xyzz* T = Tg + (size_t)id * W;
+  const G1Xyzz* T = Tg + (size_t)qi * W;
   Fq acc = quad::ld(T + W - 1, c);
   for (int w = W - 2; w >= 0; w--) {
 #pragma unroll 1
@@ -570,10 +756,18 @@ int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t*
   const int c = msm_batch_window_bits(max_terms);
   const int W = c == 5 ? BatchCfg<5>::W : BatchCfg<8>::W;
   const int WG = c == 5 ? BatchCfg<5>::WG : BatchCfg<8>::WG;
-  SV_TRY(ws->reserve(Workspace::aligned(4) + Workspace::aligned(count * W * sizeof(G1Xyzz))));
+  // SVGPU_BATCH_QUAD=0: the round-2 kernels (per-lane window sums, one-wave Horner)
+  const bool quad_path = !getenv("SVGPU_BATCH_QUAD") || atoi(getenv("SVGPU_BATCH_QUAD")) != 0;
+  const bool quad_windows = quad_path && c == kQC && max_terms <= (size_t)kQMaxTerms;
+  const size_t dig_bytes = quad_windows ? count * kQW * 2 * max_terms : 0;
+  const size_t pts_bytes = quad_windows ? count * 2 * max_terms * sizeof(G1Aff) : 0;
+  SV_TRY(ws->reserve(Workspace::aligned(4) + Workspace::aligned(count * W * sizeof(G1Xyzz)) +
+                     Workspace::aligned(dig_bytes ? dig_bytes : 1) + Workspace::aligned(pts_bytes ? pts_bytes : 1)));
   SV_TRY(ws->reserve_pinned(256));
   uint32_t* err = ws->carve<uint32_t>(1);
   G1Xyzz* Tg = ws->carve<G1Xyzz>(count * W);
+  uint8_t* dig = ws->carve<uint8_t>(dig_bytes ? dig_bytes : 1);
+  G1Aff* pts = ws->carve<G1Aff>(pts_bytes ? pts_bytes / sizeof(G1Aff) : 1);
   SV_HIP(hipMemsetAsync(err, 0, 4, st));
   const int mont = form == SV_MONTGOMERY;
   const int mont_b = (d_bidx ? base_form : form) == SV_MONTGOMERY;
@@ -581,9 +775,16 @@ int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t*
   const Fr* s = static_cast<const Fr*>(d_scalars);
   G1Aff* o = static_cast<G1Aff*>(d_out);
   const dim3 grid((uint32_t)count, WG);
-  // SVGPU_BATCH_QUAD=0: the one-wave-per-MSM Horner (LDS slots, 4 lanes) instead of the quad form
-  const bool quad_horner = !getenv("SVGPU_BATCH_QUAD") || atoi(getenv("SVGPU_BATCH_QUAD")) != 0;
-  if (c == 5) {
+  const bool quad_horner = quad_path;
+  if (quad_windows) {
+    hipLaunchKernelGGL(k_batch_prep, dim3((uint32_t)count, (uint32_t)((max_terms + kThreads - 1) / kThreads)),
+                       dim3(kThreads), 0, st, b, s, d_offsets, d_ids, mont, (uint32_t)max_terms, dig, pts, err, d_bidx,
+                       table_len, mont_b);
+    hipLaunchKernelGGL(k_batch_windows_q, dim3((uint32_t)count, (uint32_t)kQW), dim3(64), 0, st, d_offsets, d_ids,
+                       (uint32_t)max_terms, dig, pts, Tg);
+    hipLaunchKernelGGL(k_msm_batch_horner_q<5>, dim3((uint32_t)((count + 15) / 16)), dim3(64), 0, st, Tg, d_ids,
+                       (uint32_t)count, mont, o);
+  } else if (c == 5) {
     hipLaunchKernelGGL(k_msm_batch_windows<5>, grid, dim3(kThreads), 0, st, b, s, d_offsets, d_ids, mont, Tg, err,
                        d_bidx, table_len, mont_b);
     if (quad_horner)

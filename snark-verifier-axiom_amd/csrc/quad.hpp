@@ -4,7 +4,9 @@
 // one product per lane (P, R first, then PP / RR / ZZ1 ZZ2 / ZZZ1 ZZZ2, then PPP / Q / ZZ3, then
 // the two halves of Y3 and ZZZ3), the operands of each level exchanged inside the quad by DPP
 // quad_perm moves (VALU, no LDS).  Every lane runs the same instruction stream (operand choice by
-// v_cndmask), so a product costs one product of latency for the whole quad.
+// v_cndmask), so a product costs one product of latency for the whole quad.  Every perm<>() runs
+// unconditionally on all four lanes (never inside a ?: or if whose condition differs across the
+// quad: the masked-off source lane would be read as garbage).
 //
 // 2p domain as xyzz_add_2p (curve.hpp): coordinates in [0, 2p), products lazily reduced, the
 // identity exactly ZZ = 0; results are NOT canonical (fe_canon2p before a store that must be).

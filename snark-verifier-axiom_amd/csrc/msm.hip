@@ -945,7 +945,7 @@ __global__ void __launch_bounds__(kGroupBlock) k_group_sum_q(const G1Xyzz* __res
   Fq v[4] = {ps.X, ps.Y, ps.ZZ, ps.ZZZ};
   quad::transpose(v, c);
   Fq s = quad::add_2p(quad::add_2p(v[0], v[1], c), quad::add_2p(v[2], v[3], c), c);
-#pragma unroll
+#pragma unroll 1
   for (int off = 32; off >= 4; off >>= 1) {
     const Fq o = quad::down(s, off);
     if (lane < off) s = quad::add_2p(s, o, c);
@@ -954,7 +954,7 @@ __global__ void __launch_bounds__(kGroupBlock) k_group_sum_q(const G1Xyzz* __res
   __syncthreads();
   if (wave != 0) return;
   if (lane < 4 * kWaves) s = sh[lane >> 2][c];
-#pragma unroll
+#pragma unroll 1
   for (int off = 2 * kWaves; off >= 4; off >>= 1) {
     const Fq o = quad::down(s, off);
     if (lane < off) s = quad::add_2p(s, o, c);

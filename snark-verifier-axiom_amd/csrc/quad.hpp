@@ -61,6 +61,10 @@ __device__ __forceinline__ Fq dbl_2p(const Fq& a, int q) {
   return q == 0 ? X3 : (q == 1 ? Y3 : (q == 2 ? ZZ3 : ZZZ3));
 }
 
+// The rare doubling of an addition (a == b), out of line: one copy in the code instead of one per
+// inlined addition (I-cache: an unrolled tree of inlined additions outgrew it)
+__device__ __noinline__ Fq dbl_2p_cold(Fq a, int q) { return dbl_2p(a, q); }
+
 // a + b (add-2008-s, complete: identities, a == b, a == -b)
 __device__ __forceinline__ Fq add_2p(const Fq& a, const Fq& b, int q) {
   const bool odd = q & 1;
@@ -94,7 +98,7 @@ __device__ __forceinline__ Fq add_2p(const Fq& a, const Fq& b, int q) {
   const bool p0 = fe_is_zero2p(perm<qp(0, 0, 0, 0)>(d)), r0 = fe_is_zero2p(perm<qp(2, 2, 2, 2)>(d));
   const bool same = !a_id && !b_id && p0 && r0;
   if (__builtin_expect(__any(same), 0)) {  // a == b: double (wave-uniform branch, rare)
-    const Fq t = dbl_2p(a, q);
+    const Fq t = dbl_2p_cold(a, q);
     if (same) r = t;
   }
   if (!a_id && !b_id && p0 && !r0) r = Fq::zero();  // a == -b

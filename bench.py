@@ -165,11 +165,11 @@ def cpu_baseline(args, n, gpu_result, g2, sg2, accs, enc):
     cpu_s = time.perf_counter() - t0
     parity = ob.g1_from_bytes(cpu_res.tobytes()) == gpu_result
     # the same port on every core the affinity mask allows (rayon's default would take them all)
-    aff = affinity_cores()
+    aff_cores = affinity_cores()
     aff_s = None
-    if aff != threads:
+    if aff_cores != threads:
         t0 = time.perf_counter()
-        aff_res = cpu_ref.msm_pippenger(hb, hs, aff)
+        aff_res = cpu_ref.msm_pippenger(hb, hs, aff_cores)
         aff_s = time.perf_counter() - t0
         parity = parity and ob.g1_from_bytes(aff_res.tobytes()) == gpu_result
     naive = {}
@@ -210,7 +210,7 @@ def cpu_baseline(args, n, gpu_result, g2, sg2, accs, enc):
                   "config 5: accumulate 64 + one decide on 1 thread" % (args.log_n, threads, ds, len(accs), threads),
         "cpu_model": cpu_model(),
         "host_cpus_visible": os.cpu_count(),
-        "affinity_cores": aff,
+        "affinity_cores": aff_cores,
         "threads_note": "cores = min(affinity cores, OMP_NUM_THREADS share of this GPU's box slice)",
         "value_affinity_cores": n / aff_s if aff_s else n / cpu_s,
         "seconds": cpu_s,
@@ -327,10 +327,12 @@ def main():
             "x_device_resident": h_s * 1e3 / dev_ms,
             "refs_gather_inclusive_ms": r_s * 1e3,
             "refs_x_device_resident": r_s * 1e3 / dev_ms,
-            "h2d_pieces": os.environ.get("SVGPU_H2D_PIECES", "auto (2 with the GLV split, 4 without)"),
+            "h2d_pieces": os.environ.get("SVGPU_H2D_PIECES", os.environ.get(
+                "SVGPU_H2D_SPLIT", "default: 4 equal pieces (msm), 2,2,3,3,3,3 (refs)")),
             "same_result_as_device_path": bool(h_res == result and r_res == result),
-            "note": "sv_bn254_g1_msm: pageable host arrays -> HBM in pieces on a copy stream, each piece sorted and "
-                    "accumulated while the next is in flight (median of 7 calls, transfer included); "
+            "note": "sv_bn254_g1_msm: pageable host arrays -> HBM in pieces, staged back to back by the workspace's "
+                    "feeder thread; each piece sorted on a second stream once its scalars land and accumulated into "
+                    "the one bucket set once its bases land (median of 7 calls, transfer included); "
                     "sv_bn254_g1_msm_refs: 2^%d shuffled (&Fr, &G1Affine) references gathered by the library's "
                     "host pool into pinned staging, piece by piece (gather + transfer included)" % args.log_n,
         }

@@ -64,8 +64,9 @@ if os.path.exists(cal_csv):
     for k, v in calib.items():
         lines.append("| %s | %.0f | %.1f | %.3f |" % (k, v["fetch_kib"], v["known_bytes"] / 1e6, v["factor"] or 0))
 open(os.path.join(dst, f"{tag}_kernel_stats.md"), "w").write("\n".join(lines) + "\n")
-acc_f = pmc["FETCH_SIZE"].get("k_accumulate")
-acc_w = pmc["WRITE_SIZE"].get("k_accumulate")
+acc_key = next((k for k in pmc["FETCH_SIZE"] if k.startswith("k_accumulate")), None)  # k_accumulate<false> since r03
+acc_f = pmc["FETCH_SIZE"].get(acc_key) if acc_key else None
+acc_w = pmc["WRITE_SIZE"].get(acc_key) if acc_key else None
 if acc_f is not None:
     g = calib.get("gather64_64MiB", {}).get("factor")
     factor = g if g else 2.0

@@ -19,6 +19,7 @@
 // size.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -410,6 +411,171 @@ __global__ void __launch_bounds__(64) k_batch_windows_q(const uint64_t* __restri
   if (b == 0) quad::st(Tg + (size_t)k * kQW + w, c, fe_canon2p(S));
 }
 
+// ---- Steps 2 + 3, bucket-wise Horner (default for c = 5): sum_w 2^(5w) sum_b (b+1) S_wb is
+// regrouped as sum_b (b+1) H_b with H_b = sum_w 2^(5w) S_wb, so the bucket weighting (a 4-level scan
+// and a 4-level tree of quad additions) runs ONCE per MSM after the Horner instead of once per
+// window, and the window kernel only sums buckets.  The Horner then runs 16 chains per MSM (one quad
+// per bucket, one wave per MSM) instead of one: the same dependent depth, and the extra work lands
+// on SIMDs the single chain left idle.
+// bucket_window: one wave per (MSM, window): the LDS counting sort of k_batch_windows_q, then lane
+// 4b + j sums every 4th entry of bucket b from the j-th with scalar 2p-domain mixed adds (a chain of
+// ~2 adds, ~4 at most: no quad overhead while the quad's lanes hold independent work), the quad's
+// four partial sums go to quad form (quad::transpose) and are added in two levels.
+struct BucketSmem {
+  uint32_t cnt[kQB], start[kQB + 1];
+  uint16_t lst[2 * kQMaxTerms];
+};
+
+__device__ __forceinline__ void bucket_window(BucketSmem& sm, uint32_t k, uint32_t w, const uint64_t* __restrict__ off,
+                                              const uint32_t* __restrict__ ids, uint32_t max_terms,
+                                              const uint8_t* __restrict__ dig, const G1Aff* __restrict__ pts,
+                                              G1Xyzz* __restrict__ Sb) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t id = ids ? ids[k] : k;
+  const uint32_t m = (uint32_t)(off[id + 1] - off[id]);
+  const uint8_t* dg = dig + ((size_t)k * kQW + w) * 2 * (size_t)max_terms;
+  if (lane < kQB) sm.cnt[lane] = 0;
+  __syncthreads();
+  for (uint32_t j = lane; j < 2 * m; j += 64) {
+    const uint32_t d = dg[j];
+    if (d & 0x7f) atomicAdd(&sm.cnt[(d & 0x7f) - 1], 1u);
+  }
+  __syncthreads();
+  if (lane == 0) {
+    uint32_t a = 0;
+    for (int b = 0; b < kQB; b++) {
+      sm.start[b] = a;
+      a += sm.cnt[b];
+      sm.cnt[b] = sm.start[b];
+    }
+    sm.start[kQB] = a;
+  }
+  __syncthreads();
+  for (uint32_t j = lane; j < 2 * m; j += 64) {
+    const uint32_t d = dg[j];
+    if (d & 0x7f) sm.lst[atomicAdd(&sm.cnt[(d & 0x7f) - 1], 1u)] = (uint16_t)(j | ((d >> 7) << 15));
+  }
+  __syncthreads();
+  const int c = lane & 3, b = lane >> 2;
+  const G1Aff* pk = pts + 2 * (size_t)k * max_terms;
+  G1Xyzz acc = G1Xyzz::identity();
+  for (uint32_t e = sm.start[b] + c; e < sm.start[b + 1]; e += 4) {
+    const uint32_t v = sm.lst[e];
+    const uint32_t* pp = reinterpret_cast<const uint32_t*>(pk + (v & 0x7fff));
+    const Fq x = ld_fq(pp);
+    Fq y = ld_fq(pp + 8);
+    if (x.is_zero() && y.is_zero()) continue;  // identity base
+    if (v >> 15) y = -y;
+    acc = xyzz_madd_2p(acc, x, y);
+  }
+  Fq q[4] = {acc.X, acc.Y, acc.ZZ, acc.ZZZ};
+  quad::transpose(q, c);  // lane c: coordinate c of the quad's four partial sums
+  const Fq s01 = quad::add_2p(q[0], q[1], c), s23 = quad::add_2p(q[2], q[3], c);
+  quad::st(Sb + ((size_t)k * kQB + b) * kQW + w, c, fe_canon2p(quad::add_2p(s01, s23, c)));
+}
+
+// Bounded wait for a window's bucket sums (fused kernel): a wave that never sees the flag (a bug,
+// not a schedule: see k_batch_fused) raises error bit 8 and goes on, so the grid always drains
+__device__ __forceinline__ void wait_ready(const uint32_t* f, uint32_t* err) {
+  uint32_t spins = 0;
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+    __builtin_amdgcn_s_sleep(8);
+    if (++spins > (1u << 22)) {
+      if (threadIdx.x == 0) atomicOr(err, 8u);
+      break;
+    }
+  }
+}
+
+// horner_msm: one wave per MSM, quad b runs H_b = sum_w 2^(5w) S_wb (Horner, the next window's sum
+// loaded before the doublings), then sum_b (b + 1) H_b = sum_b R_b over the suffix sums R_b (scan
+// + tree as k_batch_windows_q), affine on lane 0.  kWait: window w's sums are produced by the same
+// launch (k_batch_fused), wait for its flag first.
+template <bool kWait>
+__device__ __forceinline__ void horner_msm(uint32_t k, const G1Xyzz* __restrict__ Sb, const uint32_t* __restrict__ ids,
+                                           int mont, G1Aff* __restrict__ out, const uint32_t* ready,
+                                           uint32_t* err) {
+  const int c = threadIdx.x & 3, b = threadIdx.x >> 2;
+  const uint32_t id = ids ? ids[k] : k;
+  const G1Xyzz* S = Sb + ((size_t)k * kQB + b) * kQW;
+  if (kWait) wait_ready(ready + (size_t)k * kQW + kQW - 1, err);
+  Fq acc = quad::ld(S + kQW - 1, c);
+#pragma unroll 1
+  for (int w = kQW - 2; w >= 0; w--) {
+    if (kWait) wait_ready(ready + (size_t)k * kQW + w, err);
+    const Fq nxt = quad::ld(S + w, c);
+#pragma unroll 1
+    for (int i = 0; i < kQC; i++) acc = quad::dbl_2p(acc, c);
+    acc = quad::add_2p(acc, nxt, c);
+  }
+#pragma unroll
+  for (int dq = 1; dq < kQB; dq <<= 1) {
+    const Fq o = quad::down(acc, 4 * dq);
+    if (b + dq < kQB) acc = quad::add_2p(acc, o, c);
+  }
+#pragma unroll
+  for (int dq = kQB / 2; dq >= 1; dq >>= 1) {
+    const Fq o = quad::down(acc, 4 * dq);
+    if (b < dq) acc = quad::add_2p(acc, o, c);
+  }
+  const G1Xyzz r = xyzz_canon2p(quad::gather(acc));
+  if (threadIdx.x != 0) return;
+  G1Aff a = xyzz_to_affine(r);
+  if (!mont && !r.is_identity()) {
+    a.x = fe_from_mont(a.x);
+    a.y = fe_from_mont(a.y);
+  }
+  uint32_t* o = reinterpret_cast<uint32_t*>(out + id);
+  st_fq(o, a.x);
+  st_fq(o + 8, a.y);
+}
+
+__global__ void __launch_bounds__(64) k_batch_buckets_q(const uint64_t* __restrict__ off,
+                                                        const uint32_t* __restrict__ ids, uint32_t max_terms,
+                                                        const uint8_t* __restrict__ dig,
+                                                        const G1Aff* __restrict__ pts, G1Xyzz* __restrict__ Sb) {
+  __shared__ BucketSmem sm;
+  bucket_window(sm, blockIdx.x, blockIdx.y, off, ids, max_terms, dig, pts, Sb);
+}
+
+__global__ void __launch_bounds__(64) k_batch_horner_b(const G1Xyzz* __restrict__ Sb,
+                                                       const uint32_t* __restrict__ ids, int mont,
+                                                       G1Aff* __restrict__ out) {
+  horner_msm<false>(blockIdx.x, Sb, ids, mont, out, nullptr, nullptr);
+}
+
+// Both in ONE launch, so the Horner (the batch's latency floor: ~475 dependent product levels) runs
+// while the bucket sums are still being produced: blocks [0, count) are the Horner waves (issued
+// first, raised issue priority), then bw bucket waves per MSM, wave j summing windows 25 - j,
+// 25 - j - bw, ... in the order the Horner consumes them.  (One block per (MSM, window) makes every
+// window finish at about the same time, ~0.27 ms in, and the Horner then starts from scratch.)  A bucket block publishes its window with a release flag; a Horner
+// wave waits for each window with an acquire load.  The host only takes this path while the
+// Horner waves are a small fraction of the resident-wave capacity (count <= kFuseMax), so bucket
+// blocks always find slots and every wait ends.
+constexpr uint32_t kFuseMax = 512;
+
+__global__ void __launch_bounds__(64) k_batch_fused(const uint64_t* __restrict__ off, const uint32_t* __restrict__ ids,
+                                                    uint32_t count, uint32_t max_terms,
+                                                    const uint8_t* __restrict__ dig, const G1Aff* __restrict__ pts,
+                                                    G1Xyzz* __restrict__ Sb, uint32_t* ready, uint32_t* err,
+                                                    int mont, G1Aff* __restrict__ out, uint32_t bw) {
+  __shared__ BucketSmem sm;
+  if (blockIdx.x < count) {
+    __builtin_amdgcn_s_setprio(3);
+    horner_msm<true>(blockIdx.x, Sb, ids, mont, out, ready, err);
+    return;
+  }
+  const uint32_t i = blockIdx.x - count;
+  const uint32_t k = i % count;
+  for (int w = kQW - 1 - (int)(i / count); w >= 0; w -= (int)bw) {
+    __syncthreads();
+    bucket_window(sm, k, (uint32_t)w, off, ids, max_terms, dig, pts, Sb);
+    __threadfence();
+    if (threadIdx.x == 0)
+      __hip_atomic_store(ready + (size_t)k * kQW + w, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // ---- Step 3: Horner over the window sums with the independent products of each XYZZ doubling /
 // addition issued by up to 4 lanes of one wave at once (LDS slots; 3 product levels per
 // doubling instead of 9 products, 4 per addition instead of 14).  One wave per MSM.
@@ -563,9 +729,10 @@ __global__ void __launch_bounds__(64) k_msm_batch_horner_q(const G1Xyzz* __restr
   Fq acc = quad::ld(T + W - 1, c);
 #pragma unroll 1
   for (int w = W - 2; w >= 0; w--) {
+    const Fq nxt = quad::ld(T + w, c);  // in flight during the doublings
 #pragma unroll 1
     for (int i = 0; i < C; i++) acc = quad::dbl_2p(acc, c);
-    acc = quad::add_2p(acc, quad::ld(T + w, c), c);
+    acc = quad::add_2p(acc, nxt, c);
   }
   const G1Xyzz r = xyzz_canon2p(quad::gather(acc));
   if (c != 0) return;
@@ -761,16 +928,27 @@ int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t*
   // SVGPU_BATCH_QUAD=0: the round-2 kernels (per-lane window sums, one-wave Horner)
   const bool quad_path = !getenv("SVGPU_BATCH_QUAD") || atoi(getenv("SVGPU_BATCH_QUAD")) != 0;
   const bool quad_windows = quad_path && c == kQC && max_terms <= (size_t)kQMaxTerms;
+  // bucket-wise Horner (k_batch_buckets_q + k_batch_horner_b; SVGPU_BATCH_BUCKETS=0 keeps the
+  // per-window weighting of k_batch_windows_q): 16 bucket sums per window instead of one window sum,
+  // 53 KB per MSM, so very large batches keep the per-window path
+  const bool bucket_horner = quad_windows && count <= 4096 &&
+                             (!getenv("SVGPU_BATCH_BUCKETS") || atoi(getenv("SVGPU_BATCH_BUCKETS")) != 0);
   const size_t dig_bytes = quad_windows ? count * kQW * 2 * max_terms : 0;
   const size_t pts_bytes = quad_windows ? count * 2 * max_terms * sizeof(G1Aff) : 0;
-  SV_TRY(ws->reserve(Workspace::aligned(4) + Workspace::aligned(count * W * sizeof(G1Xyzz)) +
+  const size_t nT = bucket_horner ? count * kQB * kQW : count * W;
+  // one launch for buckets + Horner while the Horner waves stay few (k_batch_fused; SVGPU_BATCH_FUSE=0
+  // runs the two kernels back to back)
+  const bool fused = bucket_horner && count <= kFuseMax &&
+                     (!getenv("SVGPU_BATCH_FUSE") || atoi(getenv("SVGPU_BATCH_FUSE")) != 0);
+  const size_t nflag = fused ? count * kQW : 0;
+  SV_TRY(ws->reserve(Workspace::aligned(4 * (1 + nflag)) + Workspace::aligned(nT * sizeof(G1Xyzz)) +
                      Workspace::aligned(dig_bytes ? dig_bytes : 1) + Workspace::aligned(pts_bytes ? pts_bytes : 1)));
   SV_TRY(ws->reserve_pinned(256));
-  uint32_t* err = ws->carve<uint32_t>(1);
-  G1Xyzz* Tg = ws->carve<G1Xyzz>(count * W);
+  uint32_t* err = ws->carve<uint32_t>(1 + nflag);  // the error word, then the window flags
+  G1Xyzz* Tg = ws->carve<G1Xyzz>(nT);
   uint8_t* dig = ws->carve<uint8_t>(dig_bytes ? dig_bytes : 1);
   G1Aff* pts = ws->carve<G1Aff>(pts_bytes ? pts_bytes / sizeof(G1Aff) : 1);
-  SV_HIP(hipMemsetAsync(err, 0, 4, st));
+  SV_HIP(hipMemsetAsync(err, 0, 4 * (1 + nflag), st));
   const int mont = form == SV_MONTGOMERY;
   const int mont_b = (d_bidx ? base_form : form) == SV_MONTGOMERY;
   const G1Aff* b = static_cast<const G1Aff*>(d_bases);
@@ -782,10 +960,20 @@ int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t*
     hipLaunchKernelGGL(k_batch_prep, dim3((uint32_t)count, (uint32_t)((max_terms + kThreads - 1) / kThreads)),
                        dim3(kThreads), 0, st, b, s, d_offsets, d_ids, mont, (uint32_t)max_terms, dig, pts, err, d_bidx,
                        table_len, mont_b);
-    hipLaunchKernelGGL(k_batch_windows_q, dim3((uint32_t)count, (uint32_t)kQW), dim3(64), 0, st, d_offsets, d_ids,
-                       (uint32_t)max_terms, dig, pts, Tg);
-    hipLaunchKernelGGL(k_msm_batch_horner_q<5>, dim3((uint32_t)((count + 15) / 16)), dim3(64), 0, st, Tg, d_ids,
-                       (uint32_t)count, mont, o);
+    if (fused) {
+      const uint32_t bw = std::min<uint32_t>(kQW, std::max(1, getenv("SVGPU_BATCH_BW") ? atoi(getenv("SVGPU_BATCH_BW")) : 4));
+      hipLaunchKernelGGL(k_batch_fused, dim3((uint32_t)(count * (1 + bw))), dim3(64), 0, st, d_offsets, d_ids,
+                         (uint32_t)count, (uint32_t)max_terms, dig, pts, Tg, err + 1, err, mont, o, bw);
+    } else if (bucket_horner) {
+      hipLaunchKernelGGL(k_batch_buckets_q, dim3((uint32_t)count, (uint32_t)kQW), dim3(64), 0, st, d_offsets, d_ids,
+                         (uint32_t)max_terms, dig, pts, Tg);
+      hipLaunchKernelGGL(k_batch_horner_b, dim3((uint32_t)count), dim3(64), 0, st, Tg, d_ids, mont, o);
+    } else {
+      hipLaunchKernelGGL(k_batch_windows_q, dim3((uint32_t)count, (uint32_t)kQW), dim3(64), 0, st, d_offsets, d_ids,
+                         (uint32_t)max_terms, dig, pts, Tg);
+      hipLaunchKernelGGL(k_msm_batch_horner_q<5>, dim3((uint32_t)((count + 15) / 16)), dim3(64), 0, st, Tg, d_ids,
+                         (uint32_t)count, mont, o);
+    }
   } else if (c == 5) {
     hipLaunchKernelGGL(k_msm_batch_windows<5>, grid, dim3(kThreads), 0, st, b, s, d_offsets, d_ids, mont, Tg, err,
                        d_bidx, table_len, mont_b);
@@ -819,6 +1007,10 @@ int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t*
   if (ev & 4u) {
     set_error("msm_batch: base index out of the table (>= %llu)", (unsigned long long)table_len);
     return SV_ERR_ARG;
+  }
+  if (ev & 8u) {
+    set_error("msm_batch: a Horner wave timed out waiting for its window sums");
+    return SV_ERR_DEVICE;
   }
   return SV_OK;
 }

@@ -488,23 +488,24 @@ static constexpr uint32_t kFineR = 18;                 // entries per thread hel
 static constexpr uint32_t kFineCap = 1024 * kFineR;    // region entries staged in LDS
 static constexpr uint32_t kChunkR = 12, kChunk = 1024 * kChunkR;  // large regions: LDS chunk
 static constexpr size_t kFineLds = (512 + 1024 + (size_t)kFineCap) * 4;  // 78 KiB: 2 blocks per CU
-template <bool BIG>
-__global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__ tmp, int e32,
-                                                    const uint32_t* __restrict__ bstart, uint32_t FB, uint32_t K,
-                                                    uint32_t* __restrict__ gst, uint32_t* __restrict__ tstart,
-                                                    uint32_t* __restrict__ ent) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t fine_lds[];
+// MODE 0: staged regions only, 1: large regions only, 2 (round 3, default): both kinds in ONE launch,
+// blocks in reverse (window, bin) order -- the crowded regions are the top window's, and as the
+// launch's first blocks they run beside the small regions instead of as a separate serial launch
+// (two launches: 37 + 35 us at 2^20, the large one a tail of a few dozen long blocks).
+// one region (window, bin) = wb: staged in LDS whole (STAGED) or in chunks
+template <bool STAGED>
+__device__ __forceinline__ void fine_region(const uint64_t* __restrict__ tmp, int e32, uint32_t wb, uint32_t s0,
+                                            uint32_t s1, uint32_t FB, uint32_t K, uint32_t* __restrict__ gst,
+                                            uint32_t* __restrict__ tstart, uint32_t* __restrict__ ent,
+                                            uint32_t* fine_lds) {
   uint32_t* fc = fine_lds;           // [512] fine-bucket counters / cursors
   uint32_t* part = fine_lds + 512;   // [1024] scan partials
   uint32_t* out = fine_lds + 1536;   // [kFineCap] the sorted region
-  const uint32_t wb = blockIdx.x, tid = threadIdx.x, NF = 1u << FB;
-  const uint32_t s0 = bstart[wb], s1 = bstart[wb + 1], len = s1 - s0;
-  if ((len > kFineCap) != BIG) return;  // block-uniform
-  constexpr bool staged = !BIG;
+  const uint32_t tid = threadIdx.x, NF = 1u << FB, len = s1 - s0;
   for (uint32_t f = tid; f < NF; f += 1024) fc[f] = 0;
   __syncthreads();
   uint64_t x[kFineR];
-  if constexpr (staged) {
+  if constexpr (STAGED) {
 #pragma unroll
     for (uint32_t r = 0; r < kFineR; r++) {
       const uint32_t i = tid + r * 1024;
@@ -542,11 +543,11 @@ __global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__
     const uint32_t st = s0 + part[tid] - v, en = st + v;
     const uint32_t g = wb * NF + tid;  // global bucket = w * B + b
     gst[g] = st;
-    fc[tid] = staged ? st - s0 : st;
+    fc[tid] = STAGED ? st - s0 : st;
     for (uint32_t t = (st + K - 1) / K; t * K < en; t++) tstart[t] = g;
   }
   __syncthreads();
-  if constexpr (staged) {
+  if constexpr (STAGED) {
 #pragma unroll
     for (uint32_t r = 0; r < kFineR; r++)
       if (tid + r * 1024 < len) out[atomicAdd(&fc[(uint32_t)(x[r] >> 32)], 1u)] = (uint32_t)x[r];
@@ -612,6 +613,24 @@ __global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__
     if (tid < NF) fc[tid] += lc[tid] - ls[tid];
     __syncthreads();
   }
+}
+
+
+// MODE 0: staged regions only, 1: large regions only, 2 (round 3, default): both kinds in ONE launch,
+// blocks in reverse (window, bin) order -- the crowded regions are the top window's, and as the
+// launch's first blocks they run beside the small regions instead of as a separate serial launch
+// (two launches: 37 + 35 us at 2^20, the large one a tail of a few dozen long blocks).
+template <int MODE>
+__global__ void __launch_bounds__(1024) k_fine_sort(const uint64_t* __restrict__ tmp, int e32,
+                                                    const uint32_t* __restrict__ bstart, uint32_t FB, uint32_t K,
+                                                    uint32_t* __restrict__ gst, uint32_t* __restrict__ tstart,
+                                                    uint32_t* __restrict__ ent) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t fine_lds[];
+  const uint32_t wb = MODE == 2 ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
+  const uint32_t s0 = bstart[wb], s1 = bstart[wb + 1];
+  const bool big = s1 - s0 > kFineCap;  // block-uniform
+  if (MODE != 1 && !big) fine_region<true>(tmp, e32, wb, s0, s1, FB, K, gst, tstart, ent, fine_lds);
+  if (MODE != 0 && big) fine_region<false>(tmp, e32, wb, s0, s1, FB, K, gst, tstart, ent, fine_lds);
 }
 
 // Each thread: K consecutive sorted entries.  See file header.
@@ -974,6 +993,159 @@ __global__ void __launch_bounds__(kGroupBlock) k_group_sum_q(const G1Xyzz* __res
   quad::st(out + gid, c, fe_canon2p(s));
 }
 
+// ---- Round 3: the subset sums as a tree inside the running-sum kernel.  k_group_sum(_q) sums every
+// group U_k = sum_{j : bit k of j} T_j from scratch: logJ groups of J/2 members, ~J logJ / 2 additions
+// per window.  The tree shares them: with block sums BS_0 = T, BS_{l+1}[i] = BS_l[2i] + BS_l[2i+1],
+// U_l = sum of the odd BS_l[i] -- ~2J additions per window (and A = sum_j acc_j).  k_wsum_tree runs
+// the running sums of 256 consecutive segments per block (one per thread, as k_wsum) and then the
+// tree of the block's 256 segments in LDS, in place: at level l the pair (2i, 2i+1) of 2^l-blocks
+// merges BS into position 2i 2^l, leaves its right half's sum at (2i + 1) 2^l as U_l's partial, and
+// merges the partials of every U_k, k < l, at offset 2^k of the two halves -- (2 + l) 2^(7-l) tasks
+// (A, BS, U_0..U_(l-1)), reads only from right halves, writes only to left halves, so a level needs
+// one barrier.  Level 0 runs in registers (lane pairs, whole additions); levels 1..7 in quad form.
+// A block ends with 10 points: A, the block total CT and U_0..U_7's partials (positions 2^k).
+// k_group_fin then sums them per window: A over the blocks (two halves, the A_lo / A_hi slots the
+// host Horner expects), U_k (k < 8) over the blocks, U_k (k >= 8) over the blocks whose index has
+// bit k - 8 set (their CT).
+static constexpr int kTreeLog = 8, kTreeN = 1 << kTreeLog;  // segments per block (= threads)
+static constexpr int kTreeRS = kTreeN + 1;                  // LDS row stride in dwords (quads conflict-free)
+static constexpr int kTreeOut = 2 + kTreeLog;               // per-block outputs
+static constexpr size_t kTreeLds = (size_t)2 * 32 * kTreeRS * 4;  // rows A and T, structure of arrays
+
+// dword d of point p at row[d * kTreeRS + p]; the quad form reads coordinate c (dwords 8c .. 8c + 7)
+__device__ __forceinline__ void tr_put(uint32_t* row, uint32_t p, const G1Xyzz& v) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(&v);
+#pragma unroll
+  for (int k = 0; k < 32; k++) row[k * kTreeRS + p] = d[k];
+}
+__device__ __forceinline__ Fq tr_getc(const uint32_t* row, uint32_t p, int c) {
+  Fq r;
+#pragma unroll
+  for (int k = 0; k < 8; k++) r.v[k] = row[(8 * c + k) * kTreeRS + p];
+  return r;
+}
+__device__ __forceinline__ void tr_putc(uint32_t* row, uint32_t p, int c, const Fq& v) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) row[(8 * c + k) * kTreeRS + p] = v.v[k];
+}
+__device__ __forceinline__ G1Xyzz xor1(const G1Xyzz& v) {  // the neighbour lane's point (DPP quad_perm)
+  G1Xyzz r;
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(&v);
+  uint32_t* o = reinterpret_cast<uint32_t*>(&r);
+#pragma unroll
+  for (int k = 0; k < 32; k++) o[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)d[k], quad::qp(1, 0, 3, 2), 0xF, 0xF, false);
+  return r;
+}
+
+__global__ void __launch_bounds__(kTreeN) k_wsum_tree(const G1Xyzz* __restrict__ X, const uint32_t* __restrict__ gst,
+                                                       uint32_t N, uint32_t J, uint32_t L,
+                                                       G1Xyzz* __restrict__ blk_out) {
+  extern __shared__ uint32_t tr_lds[];
+  uint32_t* rowA = tr_lds;
+  uint32_t* rowT = tr_lds + 32 * kTreeRS;
+  const uint32_t tid = threadIdx.x, bpw = J >> kTreeLog;
+  const uint32_t g = blockIdx.x / bpw, j = (blockIdx.x % bpw) * kTreeN + tid;
+  // running sums over segment j of window g, exactly as k_wsum with base 1
+  const G1Xyzz* x = X + (size_t)g * N;
+  const uint32_t* gs = gst ? gst + (size_t)g * N : nullptr;
+  const uint32_t lo = j * L, hi = min(N, lo + L);
+  G1Xyzz run = G1Xyzz::identity(), acc = G1Xyzz::identity();
+  if (hi > lo) {
+    uint32_t i = hi - 1;
+    G1Xyzz nx = G1Xyzz::identity();
+    bool ne = bucket_at(x, gs, i, nx);
+    for (;;) {
+      const G1Xyzz cur = nx;
+      const bool cne = ne;
+      const uint32_t ci = i;
+      if (ci > lo) {
+        i = ci - 1;
+        ne = bucket_at(x, gs, i, nx);
+      }
+      if (cne) run = xyzz_add_2p(run, cur);
+      acc = xyzz_add_2p(acc, run);
+      if (ci == lo) break;
+    }
+  }
+  // level 0 (lane pairs, one addition per lane): even lanes A[2i] + A[2i+1], odd lanes
+  // T[2i] + T[2i+1]; the odd T stays where it is as U_0's partial
+  const bool odd = tid & 1;
+  const G1Xyzz oa = xor1(acc), ot = xor1(run);
+  const G1Xyzz s0 = xyzz_add_2p(odd ? ot : acc, odd ? run : oa);
+  if (odd) {
+    tr_put(rowT, tid - 1, s0);
+    tr_put(rowT, tid, run);
+  } else {
+    tr_put(rowA, tid, s0);
+  }
+  __syncthreads();
+  // levels 1 .. 7 in quad form (a task per quad and round; tasks of one level touch disjoint slots)
+  const int c = tid & 3;
+  const uint32_t qd = tid >> 2;
+#pragma unroll 1
+  for (int l = 1; l < kTreeLog; l++) {
+    const uint32_t s = 1u << l, np = (uint32_t)kTreeN >> (l + 1), ntask = (2 + l) * np;
+#pragma unroll 1
+    for (uint32_t tau = qd; tau < ntask; tau += kTreeN / 4) {
+      uint32_t* row = rowT;
+      uint32_t dst;
+      if (tau < np) {
+        row = rowA;
+        dst = 2 * tau * s;
+      } else {
+        const uint32_t r = tau - np, kk = r / np, i = r % np;  // kk 0: BS, kk >= 1: U_(kk-1) at 2^(kk-1)
+        dst = 2 * i * s + (kk ? 1u << (kk - 1) : 0u);
+      }
+      const Fq a = tr_getc(row, dst, c), b = tr_getc(row, dst + s, c);
+      tr_putc(row, dst, c, quad::add_2p(a, b, c));
+    }
+    __syncthreads();
+  }
+  // A, CT, U_0 .. U_7 -> blk_out (2p domain; k_group_fin canonicalises)
+  if (tid < (uint32_t)kTreeOut * 4) {
+    const uint32_t q = tid >> 2;
+    const uint32_t* row = q == 0 ? rowA : rowT;
+    const uint32_t p = q < 2 ? 0u : 1u << (q - 2);
+    quad::st(blk_out + (size_t)blockIdx.x * kTreeOut + q, c, tr_getc(row, p, c));
+  }
+}
+
+// One wave per (window, output slot): at most 64 members (bpw = J / 256 <= 64), transposed into quad
+// form, two quad additions inside each quad, then the in-wave levels that still hold members.
+__global__ void __launch_bounds__(64) k_group_fin(const G1Xyzz* __restrict__ blk_out, uint32_t bpw, uint32_t NG,
+                                                  G1Xyzz* __restrict__ out) {
+  const uint32_t w = blockIdx.x / NG, q = blockIdx.x % NG, lane = threadIdx.x;
+  const int c = lane & 3;
+  const G1Xyzz* bo = blk_out + (size_t)w * bpw * kTreeOut;
+  uint32_t members, b = lane, slot;
+  if (q < 2) {  // A over the first / second half of the window's blocks
+    const uint32_t h = (bpw + 1) / 2;
+    members = q == 0 ? h : bpw - h;
+    b = (q == 0 ? 0 : h) + lane;
+    slot = 0;
+  } else if (q - 2 < (uint32_t)kTreeLog) {  // U_k, k < 8: every block's partial
+    members = bpw;
+    slot = q;
+  } else {  // U_k, k >= 8: the totals of the blocks with bit k - 8 set
+    const uint32_t m = q - 2 - kTreeLog;
+    members = bpw / 2;
+    b = ((lane >> m) << (m + 1)) | (1u << m) | (lane & ((1u << m) - 1));
+    slot = 1;
+  }
+  const G1Xyzz v = lane < members ? load_xyzz(bo, b * kTreeOut + slot) : G1Xyzz::identity();
+  Fq t[4] = {v.X, v.Y, v.ZZ, v.ZZZ};
+  quad::transpose(t, c);
+  Fq s = quad::add_2p(quad::add_2p(t[0], t[1], c), quad::add_2p(t[2], t[3], c), c);
+  const uint32_t live = (members + 3) / 4 * 4;  // lanes whose quads hold members
+#pragma unroll 1
+  for (uint32_t off = 32; off >= 4; off >>= 1) {
+    if (off >= live) continue;  // uniform: only identities above
+    const Fq o = quad::down(s, off);
+    if (lane < off) s = quad::add_2p(s, o, c);
+  }
+  if (lane < 4) quad::st(out + blockIdx.x, c, fe_canon2p(s));
+}
+
 // ---------------------------------------------------------------------------------------------
 // host orchestration
 // ---------------------------------------------------------------------------------------------
@@ -1165,27 +1337,40 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
   SV_HIP(hipGetLastError());
   if (ev_sort_mid) SV_HIP(hipEventRecord(ev_sort_mid, st));
   hipLaunchKernelGGL(k_bin_scan_chunks, dim3(nwb), dim3(kBlock), 0, st, w.bcnt, nblk, w.btot);
+  // (fusing this scan into k_bin_scan_chunks' last block -- device-scope fence + counter -- was
+  // measured 12 -> 122 us for that kernel: the fence writes back the XCD's L2)
   hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, w.btot, nwb, w.bstart, so.gst + p.nbt);
   SV_LAUNCH_C(k_bin_scatter, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.btot, w.bstart,
               w.tmp, e32);
   static thread_local int fine_attr_dev = -1;  // the > 64 KiB dynamic-LDS opt-in, once per thread/device
   if (fine_attr_dev != device) {
-    SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort<false>),
+    SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort<0>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFineLds));
-    SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort<true>),
+    SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort<1>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFineLds));
+    SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort<2>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFineLds));
     fine_attr_dev = device;
   }
-  // the two fine-sort instantiations touch disjoint regions: with a side stream the large-region
-  // one (a few dozen blocks, the top windows' crowded bins) runs concurrently with the other
+  // one launch for both region kinds (SVGPU_FINE_SPLIT=1: the round-2 pair of launches, the large
+  // regions optionally on a side stream)
+  static const bool fine_split = getenv("SVGPU_FINE_SPLIT") && atoi(getenv("SVGPU_FINE_SPLIT")) != 0;
+  if (!fine_split && !side) {
+    hipLaunchKernelGGL(k_fine_sort<2>, dim3(nwb), dim3(1024), kFineLds, st, w.tmp, e32, w.bstart, FB, so.K, so.gst,
+                       so.tstart, so.ent);
+    SV_HIP(hipGetLastError());
+    return SV_OK;
+  }
+  // the two instantiations touch disjoint regions: with a side stream the large-region one (a few
+  // dozen blocks, the top windows' crowded bins) runs concurrently with the other
   hipStream_t big_st = side ? side : st;
   if (side) {
     SV_HIP(hipEventRecord(ev_fork, st));
     SV_HIP(hipStreamWaitEvent(side, ev_fork, 0));
   }
-  hipLaunchKernelGGL(k_fine_sort<true>, dim3(nwb), dim3(1024), kFineLds, big_st, w.tmp, e32, w.bstart, FB, so.K,
+  hipLaunchKernelGGL(k_fine_sort<1>, dim3(nwb), dim3(1024), kFineLds, big_st, w.tmp, e32, w.bstart, FB, so.K,
                      so.gst, so.tstart, so.ent);
-  hipLaunchKernelGGL(k_fine_sort<false>, dim3(nwb), dim3(1024), kFineLds, st, w.tmp, e32, w.bstart, FB, so.K, so.gst,
+  hipLaunchKernelGGL(k_fine_sort<0>, dim3(nwb), dim3(1024), kFineLds, st, w.tmp, e32, w.bstart, FB, so.K, so.gst,
                      so.tstart, so.ent);
   if (side) {
     SV_HIP(hipEventRecord(ev_join, side));
@@ -1342,6 +1527,12 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   add((size_t)p.J * p.W * sizeof(G1Xyzz) * 2);  // acc_j, T_j
   add(nfinal * sizeof(G1Xyzz));                 // group sums
   add(nfinal * gparts * sizeof(G1Xyzz));        // group slice sums
+  // running sums + subset-sum tree in one kernel (k_wsum_tree) when a window's segments fill whole
+  // 256-segment blocks (at most 64 per window); SVGPU_GROUP_TREE=0 keeps k_wsum + k_group_sum(_q)
+  bool group_tree = p.J % kTreeN == 0 && p.J / kTreeN <= 64;
+  if (const char* e = getenv("SVGPU_GROUP_TREE")) group_tree = group_tree && atoi(e) != 0;
+  const size_t ntree = group_tree ? (size_t)p.W * (p.J / kTreeN) * kTreeOut : 0;
+  add(ntree * sizeof(G1Xyzz));                  // per-block tree outputs
   SV_TRY(ws->reserve(bytes));
   SV_TRY(ws->reserve_pinned(nfinal * sizeof(G1Xyzz) + 256));
   if (feed) {
@@ -1378,6 +1569,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   G1Xyzz* racc = ws->carve<G1Xyzz>((size_t)p.J * p.W);
   G1Xyzz* rtot = ws->carve<G1Xyzz>((size_t)p.J * p.W);
   G1Xyzz* gpart = ws->carve<G1Xyzz>(nfinal * gparts);
+  G1Xyzz* tree_out = group_tree ? ws->carve<G1Xyzz>(ntree) : nullptr;
   {
     uint64_t eo = 0, to = 0;
     for (int k = 0; k < pieces; k++) {
@@ -1519,15 +1711,27 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   // several host-fed pieces every bucket of bsum holds a value: no emptiness table).  (Reducing the top windows
   // first to overlap the host Horner with the lower ones was measured slower: each half-size launch
   // of these occupancy-bound kernels takes nearly as long as the whole -- reduce 0.40 -> 0.67 ms.)
-  hipLaunchKernelGGL(k_wsum, dim3(cdiv((uint64_t)p.J * p.W, kBlock)), dim3(kBlock), 0, st, bsum,
-                     pieces > 1 ? nullptr : so[0].gst, p.B, p.J, 1u << p.logL, p.W, 1, racc, rtot);
   const bool group_quad = !getenv("SVGPU_GROUP_QUAD") || atoi(getenv("SVGPU_GROUP_QUAD")) != 0;
-  if (group_quad)
-    hipLaunchKernelGGL(k_group_sum_q, dim3(p.NG * p.W * gparts), dim3(kGroupBlock), 0, st, racc, rtot, p.J, p.logJ,
-                       gparts, ping, gpart, w.err + 64);
-  else
-    hipLaunchKernelGGL(k_group_sum, dim3(p.NG * p.W * gparts), dim3(kGroupBlock), 0, st, racc, rtot, p.J, p.logJ,
-                       gparts, ping, gpart, w.err + 64);
+  if (group_tree) {
+    static thread_local int tree_attr_dev = -1;  // the > 64 KiB dynamic-LDS opt-in, once per thread/device
+    if (tree_attr_dev != device) {
+      SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wsum_tree),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTreeLds));
+      tree_attr_dev = device;
+    }
+    hipLaunchKernelGGL(k_wsum_tree, dim3(p.J / kTreeN * p.W), dim3(kTreeN), kTreeLds, st, bsum,
+                       pieces > 1 ? nullptr : so[0].gst, p.B, p.J, 1u << p.logL, tree_out);
+    hipLaunchKernelGGL(k_group_fin, dim3(p.W * p.NG), dim3(64), 0, st, tree_out, p.J / kTreeN, p.NG, ping);
+  } else {
+    hipLaunchKernelGGL(k_wsum, dim3(cdiv((uint64_t)p.J * p.W, kBlock)), dim3(kBlock), 0, st, bsum,
+                       pieces > 1 ? nullptr : so[0].gst, p.B, p.J, 1u << p.logL, p.W, 1, racc, rtot);
+    if (group_quad)
+      hipLaunchKernelGGL(k_group_sum_q, dim3(p.NG * p.W * gparts), dim3(kGroupBlock), 0, st, racc, rtot, p.J,
+                         p.logJ, gparts, ping, gpart, w.err + 64);
+    else
+      hipLaunchKernelGGL(k_group_sum, dim3(p.NG * p.W * gparts), dim3(kGroupBlock), 0, st, racc, rtot, p.J,
+                         p.logJ, gparts, ping, gpart, w.err + 64);
+  }
   SV_HIP(hipGetLastError());
   if (!lean) SV_HIP(hipEventRecord(ev[5], st));
   SV_HIP(hipMemcpyAsync(ws->pinned, ping, nfinal * sizeof(G1Xyzz) + 4, hipMemcpyDeviceToHost, st));

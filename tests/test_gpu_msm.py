@@ -231,3 +231,33 @@ def test_glv_phi_table_layouts(gpu, oracle_cpp, n, phi64, monkeypatch):
     B[n // 2] = 0  # identity (0, 0) maps to itself under phi
     exp = _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
     assert svgpu.msm_arrays(B, S, svgpu.SV_CANONICAL) == exp
+
+
+@pytest.mark.parametrize("path", ["tree", "quad", "plain"])
+@pytest.mark.parametrize("glv", ["0", "1"])
+def test_bucket_reduction_paths(gpu, oracle_cpp, monkeypatch, path, glv):
+    """The three bucket reductions -- running sums + in-block subset-sum tree (k_wsum_tree +
+    k_group_fin, the default once a window has >= 256 segments), and k_wsum with the quad-form or
+    whole-addition group sums -- give the reference Pippenger's point (msm.rs:238-316), on dense
+    random scalars and on sparse ones whose windows leave most buckets / segments / tree blocks empty
+    (identity partials at every tree level), device-resident and host-fed."""
+    import svgpu
+    from svgpu import encoding as enc
+    monkeypatch.setenv("SVGPU_GLV", glv)
+    monkeypatch.setenv("SVGPU_GROUP_TREE", "1" if path == "tree" else "0")
+    monkeypatch.setenv("SVGPU_GROUP_QUAD", "0" if path == "plain" else "1")
+    for n, start in ((1 << 16, 5), (70001, 9)):
+        B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=start)
+        S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=start)
+        assert svgpu.msm_arrays(B, S) == _to_pt(oracle_cpp.msm_pippenger(B, S, 0)), (n, "dense")
+    # sparse: small scalars (only the lowest windows' low buckets) and a few huge ones
+    n = 1 << 16
+    B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=3)
+    rng = np.random.default_rng(11)
+    sc = [int(x) for x in rng.integers(0, 1 << 12, n)]
+    for i in range(0, n, 4099):
+        sc[i] = b.R - 1 - i
+    S = enc.scalars_array(sc)
+    assert svgpu.msm_arrays(B, S) == _to_pt(oracle_cpp.msm_pippenger(B, S, 0)), "sparse"
+    monkeypatch.setenv("SVGPU_H2D_PIECES", "3")
+    assert svgpu.msm_arrays(B, S) == _to_pt(oracle_cpp.msm_pippenger(B, S, 0)), "sparse host-fed"

@@ -220,8 +220,12 @@ int sv_bn254_g1_msm(const sv_g1_affine* bases, const sv_fe* scalars, size_t n, i
   SV_GUARD_END
 }
 
-// references gathered this far ahead are prefetched (random 32/64-B reads are DRAM-latency bound)
-static constexpr size_t kGatherAhead = 16;
+// references gathered this far ahead are prefetched (random 32/64-B reads are DRAM-latency bound);
+// SVGPU_GATHER_AHEAD overrides (read once)
+static size_t gather_ahead() {
+  static const size_t a = getenv("SVGPU_GATHER_AHEAD") ? (size_t)std::max(1, atoi(getenv("SVGPU_GATHER_AHEAD"))) : 16;
+  return a;
+}
 
 int sv_bn254_g1_msm_refs(const sv_msm_ref* pairs, size_t n, int form, int num_gpus, sv_g1_affine* out) noexcept {
   SV_GUARD_BEGIN
@@ -260,6 +264,7 @@ int sv_bn254_g1_msm_refs(const sv_msm_ref* pairs, size_t n, int form, int num_gp
     // sort overlap the base gather, and this piece's DMA the next piece's gather).  (Gathering both
     // in one pass per piece was measured slower: 3.7 -> 4.2-4.9 ms at 2^20, the sort then waits for
     // the whole piece.)
+    const size_t kGatherAhead = gather_ahead();
     feed.stage_scalars = [&, lo](size_t a, size_t b, void* ds, hipStream_t cs, hipEvent_t ready) -> int {
       host_parallel_for(b - a, 8192, [&](size_t x, size_t y) {
         for (size_t i = a + x; i < a + y; i++) {

@@ -50,7 +50,7 @@ namespace sv {
 
 static constexpr int kBlock = 256;
 #ifndef SV_ACC_PREFETCH
-#define SV_ACC_PREFETCH 1  // next entry index loaded a step ahead (0: none, 2: next point too -- 138 VGPRs, no gain)
+#define SV_ACC_PREFETCH 1  // next entry index loaded a step ahead (0: none, 2: next point too -- 162 VGPRs, no gain)
 #endif
 
 __device__ __forceinline__ G1Aff load_aff(const G1Aff* __restrict__ a, uint32_t i) {
@@ -647,7 +647,7 @@ __device__ __forceinline__ bool join_in_block(uint32_t gs, uint32_t ge, uint32_t
   const uint32_t t0 = gs / K, t1 = (ge - 1) / K;
   return t1 == t0 + 1 && t0 / kBlock == t1 / kBlock;
 }
-template <bool ADD>
+template <bool ADD, int PF = SV_ACC_PREFETCH>
 __global__ void __launch_bounds__(kBlock) k_accumulate(
     const G1Aff* __restrict__ bases, const uint32_t* __restrict__ ent, const uint32_t* __restrict__ gst,
     const uint32_t* __restrict__ tstart, uint32_t nbt, uint32_t K, uint32_t T,
@@ -676,16 +676,10 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
     if constexpr (ADD) {
       if (s0 == gs) acc = load_xyzz(bsum, g);
     }
-#if SV_ACC_PREFETCH >= 1
-    uint32_t vnext = ent[s0];
-#endif
-#if SV_ACC_PREFETCH >= 2
+    uint32_t vnext = 0;
+    if constexpr (PF >= 1) vnext = ent[s0];
     G1Aff pnext;
-    {
-      const uint32_t idx = vnext & 0x7fffffffu;
-      pnext = load_vpoint(bases, phix, idx, nsplit, phi64);
-    }
-#endif
+    if constexpr (PF >= 2) pnext = load_vpoint(bases, phix, vnext & 0x7fffffffu, nsplit, phi64);
     for (uint32_t e = s0; e < e_end; e++) {
       if (e >= ge) {  // segment [seg_start, ge) of bucket g ends inside this chunk
         acc = xyzz_canon2p(acc);
@@ -706,22 +700,23 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(
         if constexpr (ADD) acc = load_xyzz(bsum, g);
         else acc = G1Xyzz::identity();
       }
-#if SV_ACC_PREFETCH == 0
-      const uint32_t v = ent[e], idx = v & 0x7fffffffu;
-      G1Aff p = load_vpoint(bases, phix, idx, nsplit, phi64);
-#elif SV_ACC_PREFETCH == 1
-      const uint32_t v = vnext, idx = v & 0x7fffffffu;
-      if (e + 1 < e_end) vnext = ent[e + 1];
-      G1Aff p = load_vpoint(bases, phix, idx, nsplit, phi64);
-#else
-      const uint32_t v = vnext;
-      G1Aff p = pnext;
-      if (e + 1 < e_end) {  // next entry's point in flight during this addition
-        vnext = ent[e + 1];
-        const uint32_t idx = vnext & 0x7fffffffu;
-        pnext = load_vpoint(bases, phix, idx, nsplit, phi64);
+      uint32_t v;
+      G1Aff p;
+      if constexpr (PF == 0) {
+        v = ent[e];
+        p = load_vpoint(bases, phix, v & 0x7fffffffu, nsplit, phi64);
+      } else if constexpr (PF == 1) {
+        v = vnext;
+        if (e + 1 < e_end) vnext = ent[e + 1];
+        p = load_vpoint(bases, phix, v & 0x7fffffffu, nsplit, phi64);
+      } else {
+        v = vnext;
+        p = pnext;
+        if (e + 1 < e_end) {  // next entry's point in flight during this addition
+          vnext = ent[e + 1];
+          pnext = load_vpoint(bases, phix, vnext & 0x7fffffffu, nsplit, phi64);
+        }
       }
-#endif
       if (v & 0x80000000u) p.y = -p.y;
       if (!p.is_identity()) acc = xyzz_madd_2p(acc, p.x, p.y);
     }
@@ -1386,14 +1381,16 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
 static int msm_acc(const MsmPlan& p, const MsmScratch& w, const SortOut& so, const G1Aff* bases, int add_into,
                    hipStream_t st, G1Xyzz* bsum, const uint4* phix, uint32_t nsplit, hipEvent_t ev_acc_done,
                    hipEvent_t ev_fix_mid) {
+  // (a point prefetch one entry ahead, k_accumulate<., 2>, measured no gain on the device path or
+  // on the host-fed pieces' ~2 waves per SIMD: 2^20 host-fed 2.69-2.71 ms either way)
   if (add_into)
-    hipLaunchKernelGGL(k_accumulate<true>, dim3(cdiv(so.T, kBlock)), dim3(kBlock), 0, st, bases, so.ent, so.gst,
-                       so.tstart, p.nbt, so.K, so.T, bsum, w.pfirst, w.plast, w.multi, w.nmulti, w.heavy, w.nheavy,
-                       phix, nsplit, p.phi64);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_accumulate<true>), dim3(cdiv(so.T, kBlock)), dim3(kBlock), 0, st, bases,
+                       so.ent, so.gst, so.tstart, p.nbt, so.K, so.T, bsum, w.pfirst, w.plast, w.multi, w.nmulti,
+                       w.heavy, w.nheavy, phix, nsplit, p.phi64);
   else
-    hipLaunchKernelGGL(k_accumulate<false>, dim3(cdiv(so.T, kBlock)), dim3(kBlock), 0, st, bases, so.ent, so.gst,
-                       so.tstart, p.nbt, so.K, so.T, bsum, w.pfirst, w.plast, w.multi, w.nmulti, w.heavy, w.nheavy,
-                       phix, nsplit, p.phi64);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_accumulate<false>), dim3(cdiv(so.T, kBlock)), dim3(kBlock), 0, st, bases,
+                       so.ent, so.gst, so.tstart, p.nbt, so.K, so.T, bsum, w.pfirst, w.plast, w.multi, w.nmulti,
+                       w.heavy, w.nheavy, phix, nsplit, p.phi64);
   SV_HIP(hipGetLastError());
   if (ev_acc_done) SV_HIP(hipEventRecord(ev_acc_done, st));
   const uint32_t gm = std::min<uint32_t>(cdiv(p.nbt, kBlock), 1024);
@@ -1626,6 +1623,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
     // accumulates the piece into the one bucket set (identity-initialised; pieces after the first
     // add into it).
     hipStream_t cs = ws->copy_stream, ss = ws->sort_stream;
+    const bool prep_on_sort = !getenv("SVGPU_FED_PREP") || atoi(getenv("SVGPU_FED_PREP")) != 0;
     if (pieces > 1) SV_HIP(hipMemsetAsync(bsum, 0, (size_t)p.nbt * sizeof(G1Xyzz), st));
     SV_HIP(hipEventRecord(ev[6], st));
     SV_HIP(hipStreamWaitEvent(cs, ev[6], 0));
@@ -1683,19 +1681,25 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
       SV_TRY(wait_stage(2 * k + 1));
       SV_HIP(hipStreamWaitEvent(ss, sc_ready, 0));
       SV_TRY(msm_sort(p, w, so[k], nullptr, dsc, m, mont_in, device, ss, nullptr, nsplit, 0, nullptr));
-      SV_HIP(hipEventRecord(sorted, ss));
+      if (!prep_on_sort) SV_HIP(hipEventRecord(sorted, ss));
       SV_TRY(wait_stage(2 * k + 2));
-      SV_HIP(hipStreamWaitEvent(st, b_ready, 0));
+      // the landed bases' preparation (conversion / check / the piece's phi table) runs on the sort
+      // stream behind the piece's sort (round 3: off the compute stream, whose back-to-back
+      // accumulates are the host-fed path's critical path once the first piece has landed);
+      // SVGPU_FED_PREP=0 keeps it on the compute stream
+      hipStream_t ps = prep_on_sort ? ss : st;
+      SV_HIP(hipStreamWaitEvent(ps, b_ready, 0));
       const G1Aff* pbases = conv ? bases_m + lo : db;
       if (conv)  // canonical bases converted (and checked) once they have landed
-        hipLaunchKernelGGL(k_to_mont_bases, dim3(cdiv(m, kBlock)), dim3(kBlock), 0, st, db, bases_m + lo,
+        hipLaunchKernelGGL(k_to_mont_bases, dim3(cdiv(m, kBlock)), dim3(kBlock), 0, ps, db, bases_m + lo,
                            (uint32_t)m, w.err);
       else if (!p.glv)
-        hipLaunchKernelGGL(k_check_bases, dim3(cdiv(m, kBlock)), dim3(kBlock), 0, st, db, (uint32_t)m, w.err);
+        hipLaunchKernelGGL(k_check_bases, dim3(cdiv(m, kBlock)), dim3(kBlock), 0, ps, db, (uint32_t)m, w.err);
       if (p.glv)  // the piece's phi table from the landed (converted) bases; Montgomery ones checked
-        hipLaunchKernelGGL(k_glv_phix, dim3(cdiv(m, kBlock)), dim3(kBlock), 0, st, pbases, (uint32_t)m, phix_k,
+        hipLaunchKernelGGL(k_glv_phix, dim3(cdiv(m, kBlock)), dim3(kBlock), 0, ps, pbases, (uint32_t)m, phix_k,
                            p.phi64, conv ? nullptr : w.err);
       SV_HIP(hipGetLastError());
+      if (prep_on_sort) SV_HIP(hipEventRecord(sorted, ss));
       SV_HIP(hipStreamWaitEvent(st, sorted, 0));
       if (k == 0) SV_HIP(hipEventRecord(ev[2], st));
       // each piece has its own fixup queue counters (err[1 + 2k], err[2 + 2k], zeroed with the

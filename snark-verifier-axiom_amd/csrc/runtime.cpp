@@ -83,6 +83,9 @@ int Workspace::reserve_in(size_t bytes) {
   return SV_OK;
 }
 
+// Gather staging of sv_bn254_g1_msm_refs: pinned.  (Measured round 3 at 2^20, shuffled refs:
+// pinned 3.00 ms, pageable staging through the runtime's own copy path 5.4 ms, pinned non-coherent
+// 5.3 ms.)
 int Workspace::reserve_stage(size_t bytes) {
   if (bytes <= stage_cap) return SV_OK;
   if (stage) {

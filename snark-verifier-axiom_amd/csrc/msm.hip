@@ -1005,13 +1005,20 @@ __global__ void __launch_bounds__(kGroupBlock) k_group_sum_q(const G1Xyzz* __res
 static constexpr int kTreeLog = 8, kTreeN = 1 << kTreeLog;  // segments per block (= threads)
 static constexpr int kTreeRS = kTreeN + 1;                  // LDS row stride in dwords (quads conflict-free)
 static constexpr int kTreeOut = 2 + kTreeLog;               // per-block outputs
-static constexpr size_t kTreeLds = (size_t)2 * 32 * kTreeRS * 4;  // rows A and T, structure of arrays
+static constexpr size_t kTreeRow = (size_t)32 * kTreeRS * 4;  // one row of 256 points, structure of arrays
 
 // dword d of point p at row[d * kTreeRS + p]; the quad form reads coordinate c (dwords 8c .. 8c + 7)
 __device__ __forceinline__ void tr_put(uint32_t* row, uint32_t p, const G1Xyzz& v) {
   const uint32_t* d = reinterpret_cast<const uint32_t*>(&v);
 #pragma unroll
   for (int k = 0; k < 32; k++) row[k * kTreeRS + p] = d[k];
+}
+__device__ __forceinline__ G1Xyzz tr_get(const uint32_t* row, uint32_t p) {
+  G1Xyzz v;
+  uint32_t* d = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+  for (int k = 0; k < 32; k++) d[k] = row[k * kTreeRS + p];
+  return v;
 }
 __device__ __forceinline__ Fq tr_getc(const uint32_t* row, uint32_t p, int c) {
   Fq r;
@@ -1031,73 +1038,105 @@ __device__ __forceinline__ G1Xyzz xor1(const G1Xyzz& v) {  // the neighbour lane
   for (int k = 0; k < 32; k++) o[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)d[k], quad::qp(1, 0, 3, 2), 0xF, 0xF, false);
   return r;
 }
+// task tau of tree level l (pairs of 2^l-blocks, np pairs, A row first when RUN): its row and the
+// left-half slot it merges into (the right half's slot is + 2^l)
+template <bool RUN>
+__device__ __forceinline__ uint32_t* tr_task(uint32_t tau, uint32_t np, uint32_t s, uint32_t* rowA, uint32_t* rowT,
+                                             uint32_t& dst) {
+  if (RUN && tau < np) {
+    dst = 2 * tau * s;
+    return rowA;
+  }
+  const uint32_t r = RUN ? tau - np : tau, kk = r / np, i = r % np;  // kk 0: BS, kk >= 1: U_(kk-1) at 2^(kk-1)
+  dst = 2 * i * s + (kk ? 1u << (kk - 1) : 0u);
+  return rowT;
+}
 
+// RUN: running sums over L-bucket segments, then the tree over the block's 256 segments (rows A and
+// T; one block per CU at 2^20).  !RUN (round 3, L = 1): the tree straight over 256 buckets per block
+// -- no running sums and no A row (A = the total), a quarter of the LDS, so four blocks share a CU
+// and one block's latency-bound upper levels overlap another's wide lower ones; its wide levels
+// 1 and 2 run as whole additions (one per lane), the rest in quad form.
+template <bool RUN>
 __global__ void __launch_bounds__(kTreeN) k_wsum_tree(const G1Xyzz* __restrict__ X, const uint32_t* __restrict__ gst,
                                                        uint32_t N, uint32_t J, uint32_t L,
                                                        G1Xyzz* __restrict__ blk_out) {
   extern __shared__ uint32_t tr_lds[];
-  uint32_t* rowA = tr_lds;
-  uint32_t* rowT = tr_lds + 32 * kTreeRS;
+  uint32_t* rowT = tr_lds;
+  uint32_t* rowA = tr_lds + 32 * kTreeRS;  // RUN only
+  constexpr int kWhole = RUN ? 1 : 3;      // levels below this run as whole additions
   const uint32_t tid = threadIdx.x, bpw = J >> kTreeLog;
   const uint32_t g = blockIdx.x / bpw, j = (blockIdx.x % bpw) * kTreeN + tid;
-  // running sums over segment j of window g, exactly as k_wsum with base 1
   const G1Xyzz* x = X + (size_t)g * N;
   const uint32_t* gs = gst ? gst + (size_t)g * N : nullptr;
-  const uint32_t lo = j * L, hi = min(N, lo + L);
-  G1Xyzz run = G1Xyzz::identity(), acc = G1Xyzz::identity();
-  if (hi > lo) {
-    uint32_t i = hi - 1;
-    G1Xyzz nx = G1Xyzz::identity();
-    bool ne = bucket_at(x, gs, i, nx);
-    for (;;) {
-      const G1Xyzz cur = nx;
-      const bool cne = ne;
-      const uint32_t ci = i;
-      if (ci > lo) {
-        i = ci - 1;
-        ne = bucket_at(x, gs, i, nx);
+  const bool odd = tid & 1;
+  if constexpr (RUN) {
+    // running sums over segment j of window g, exactly as k_wsum with base 1
+    const uint32_t lo = j * L, hi = min(N, lo + L);
+    G1Xyzz run = G1Xyzz::identity(), acc = G1Xyzz::identity();
+    if (hi > lo) {
+      uint32_t i = hi - 1;
+      G1Xyzz nx = G1Xyzz::identity();
+      bool ne = bucket_at(x, gs, i, nx);
+      for (;;) {
+        const G1Xyzz cur = nx;
+        const bool cne = ne;
+        const uint32_t ci = i;
+        if (ci > lo) {
+          i = ci - 1;
+          ne = bucket_at(x, gs, i, nx);
+        }
+        if (cne) run = xyzz_add_2p(run, cur);
+        acc = xyzz_add_2p(acc, run);
+        if (ci == lo) break;
       }
-      if (cne) run = xyzz_add_2p(run, cur);
-      acc = xyzz_add_2p(acc, run);
-      if (ci == lo) break;
+    }
+    // level 0 (lane pairs, one addition per lane): even lanes A[2i] + A[2i+1], odd lanes
+    // T[2i] + T[2i+1]; the odd T stays where it is as U_0's partial
+    const G1Xyzz oa = xor1(acc), ot = xor1(run);
+    const G1Xyzz s0 = xyzz_add_2p(odd ? ot : acc, odd ? run : oa);
+    if (odd) {
+      tr_put(rowT, tid - 1, s0);
+      tr_put(rowT, tid, run);
+    } else {
+      tr_put(rowA, tid, s0);
+    }
+  } else {
+    // level 0 over the buckets themselves (odd lanes; an empty bucket is the identity)
+    G1Xyzz t = G1Xyzz::identity();
+    if (j < N) bucket_at(x, gs, j, t);
+    const G1Xyzz ot = xor1(t);
+    if (odd) {
+      tr_put(rowT, tid - 1, xyzz_add_2p(ot, t));
+      tr_put(rowT, tid, t);
     }
   }
-  // level 0 (lane pairs, one addition per lane): even lanes A[2i] + A[2i+1], odd lanes
-  // T[2i] + T[2i+1]; the odd T stays where it is as U_0's partial
-  const bool odd = tid & 1;
-  const G1Xyzz oa = xor1(acc), ot = xor1(run);
-  const G1Xyzz s0 = xyzz_add_2p(odd ? ot : acc, odd ? run : oa);
-  if (odd) {
-    tr_put(rowT, tid - 1, s0);
-    tr_put(rowT, tid, run);
-  } else {
-    tr_put(rowA, tid, s0);
-  }
   __syncthreads();
-  // levels 1 .. 7 in quad form (a task per quad and round; tasks of one level touch disjoint slots)
   const int c = tid & 3;
   const uint32_t qd = tid >> 2;
 #pragma unroll 1
   for (int l = 1; l < kTreeLog; l++) {
-    const uint32_t s = 1u << l, np = (uint32_t)kTreeN >> (l + 1), ntask = (2 + l) * np;
-#pragma unroll 1
-    for (uint32_t tau = qd; tau < ntask; tau += kTreeN / 4) {
-      uint32_t* row = rowT;
-      uint32_t dst;
-      if (tau < np) {
-        row = rowA;
-        dst = 2 * tau * s;
-      } else {
-        const uint32_t r = tau - np, kk = r / np, i = r % np;  // kk 0: BS, kk >= 1: U_(kk-1) at 2^(kk-1)
-        dst = 2 * i * s + (kk ? 1u << (kk - 1) : 0u);
+    const uint32_t s = 1u << l, np = (uint32_t)kTreeN >> (l + 1), ntask = ((RUN ? 2 : 1) + l) * np;
+    if (l < kWhole) {  // whole additions, one task per thread (ntask <= 256)
+      if (tid < ntask) {
+        uint32_t dst;
+        uint32_t* row = tr_task<RUN>(tid, np, s, rowA, rowT, dst);
+        const G1Xyzz a = tr_get(row, dst), b = tr_get(row, dst + s);
+        tr_put(row, dst, xyzz_add_2p(a, b));
       }
-      const Fq a = tr_getc(row, dst, c), b = tr_getc(row, dst + s, c);
-      tr_putc(row, dst, c, quad::add_2p(a, b, c));
+    } else {  // quad form: a task per quad and round (tasks of one level touch disjoint slots)
+#pragma unroll 1
+      for (uint32_t tau = qd; tau < ntask; tau += kTreeN / 4) {
+        uint32_t dst;
+        uint32_t* row = tr_task<RUN>(tau, np, s, rowA, rowT, dst);
+        const Fq a = tr_getc(row, dst, c), b = tr_getc(row, dst + s, c);
+        tr_putc(row, dst, c, quad::add_2p(a, b, c));
+      }
     }
     __syncthreads();
   }
-  // A, CT, U_0 .. U_7 -> blk_out (2p domain; k_group_fin canonicalises)
-  if (tid < (uint32_t)kTreeOut * 4) {
+  // [A,] CT, U_0 .. U_7 -> blk_out (2p domain; k_group_fin canonicalises)
+  if (tid >= (RUN ? 0u : 4u) && tid < (uint32_t)kTreeOut * 4) {
     const uint32_t q = tid >> 2;
     const uint32_t* row = q == 0 ? rowA : rowT;
     const uint32_t p = q < 2 ? 0u : 1u << (q - 2);
@@ -1105,38 +1144,51 @@ __global__ void __launch_bounds__(kTreeN) k_wsum_tree(const G1Xyzz* __restrict__
   }
 }
 
-// One wave per (window, output slot): at most 64 members (bpw = J / 256 <= 64), transposed into quad
-// form, two quad additions inside each quad, then the in-wave levels that still hold members.
-__global__ void __launch_bounds__(64) k_group_fin(const G1Xyzz* __restrict__ blk_out, uint32_t bpw, uint32_t NG,
-                                                  G1Xyzz* __restrict__ out) {
-  const uint32_t w = blockIdx.x / NG, q = blockIdx.x % NG, lane = threadIdx.x;
+// One block of two waves per (window, output slot): up to 128 members (bpw = J / 256 <= 128), each
+// wave's 64 transposed into quad form, two quad additions inside each quad, the in-wave levels that
+// still hold members, then wave 1's sum added to wave 0's.  aslot: the per-block slot the A sums
+// read (0: A with running sums, 1: the block total CT for the pure tree).
+__global__ void __launch_bounds__(128) k_group_fin(const G1Xyzz* __restrict__ blk_out, uint32_t bpw, uint32_t NG,
+                                                   uint32_t aslot, G1Xyzz* __restrict__ out) {
+  __shared__ Fq sh[4];
+  const uint32_t w = blockIdx.x / NG, q = blockIdx.x % NG, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int c = lane & 3;
   const G1Xyzz* bo = blk_out + (size_t)w * bpw * kTreeOut;
-  uint32_t members, b = lane, slot;
+  uint32_t members, b = tid, slot;
   if (q < 2) {  // A over the first / second half of the window's blocks
     const uint32_t h = (bpw + 1) / 2;
     members = q == 0 ? h : bpw - h;
-    b = (q == 0 ? 0 : h) + lane;
-    slot = 0;
+    b = (q == 0 ? 0 : h) + tid;
+    slot = aslot;
   } else if (q - 2 < (uint32_t)kTreeLog) {  // U_k, k < 8: every block's partial
     members = bpw;
     slot = q;
   } else {  // U_k, k >= 8: the totals of the blocks with bit k - 8 set
     const uint32_t m = q - 2 - kTreeLog;
     members = bpw / 2;
-    b = ((lane >> m) << (m + 1)) | (1u << m) | (lane & ((1u << m) - 1));
+    b = ((tid >> m) << (m + 1)) | (1u << m) | (tid & ((1u << m) - 1));
     slot = 1;
   }
-  const G1Xyzz v = lane < members ? load_xyzz(bo, b * kTreeOut + slot) : G1Xyzz::identity();
+  if (wv > 0 && wv * 64 >= members) return;  // wave 1 only when there are more than 64 (wave 0 always
+                                              // stores, the identity for an empty slot)
+  const G1Xyzz v = tid < members ? load_xyzz(bo, b * kTreeOut + slot) : G1Xyzz::identity();
   Fq t[4] = {v.X, v.Y, v.ZZ, v.ZZZ};
   quad::transpose(t, c);
   Fq s = quad::add_2p(quad::add_2p(t[0], t[1], c), quad::add_2p(t[2], t[3], c), c);
-  const uint32_t live = (members + 3) / 4 * 4;  // lanes whose quads hold members
+  const uint32_t wm = min(64u, members - wv * 64);
+  const uint32_t live = (wm + 3) / 4 * 4;  // lanes whose quads hold members
 #pragma unroll 1
   for (uint32_t off = 32; off >= 4; off >>= 1) {
     if (off >= live) continue;  // uniform: only identities above
     const Fq o = quad::down(s, off);
     if (lane < off) s = quad::add_2p(s, o, c);
+  }
+  if (members > 64) {
+    if (wv == 1 && lane < 4) sh[c] = s;
+    __syncthreads();
+    if (wv == 1) return;
+    const Fq o = sh[c];
+    s = quad::add_2p(s, o, c);
   }
   if (lane < 4) quad::st(out + blockIdx.x, c, fe_canon2p(s));
 }
@@ -1223,7 +1275,16 @@ MsmPlan msm_plan(size_t n) {
   if (const char* e = getenv("SVGPU_RED_LOG")) p.logL = atoi(e);
   if (p.logL < 1) p.logL = 1;
   if (p.logL > p.c - 3) p.logL = p.c - 3 > 1 ? p.c - 3 : 1;
+  // bucket reduction (SVGPU_GROUP_TREE): 1 (default) running sums + in-block subset-sum tree
+  // (k_wsum_tree<true>) when a window's segments fill whole 256-segment blocks, at most 64 of them;
+  // 2 the tree straight over the buckets (k_wsum_tree<false>, no running sums: L = 1); 0 k_wsum +
+  // k_group_sum(_q)
+  p.tree = 1;
+  if (const char* e = getenv("SVGPU_GROUP_TREE")) p.tree = atoi(e);
+  if (p.tree == 2 && p.B % kTreeN == 0 && p.B / kTreeN <= 128) p.logL = 0;
+  else if (p.tree == 2) p.tree = 1;
   p.J = p.B >> p.logL;
+  if (p.tree == 1 && !(p.J % kTreeN == 0 && p.J / kTreeN <= 64)) p.tree = 0;
   p.logJ = 0;
   while ((1u << p.logJ) < p.J) p.logJ++;
   p.NG = 2 + p.logJ;
@@ -1285,11 +1346,9 @@ static host::Xyzz host_combine(const MsmPlan& p, const host::Xyzz* A) {
     acc = host::x_dbl(acc);
     const uint32_t w = (uint32_t)e / p.c, r = (uint32_t)e % p.c;
     const host::Xyzz* a = A + w * p.NG;
-    if (r == 0) {
-      acc = host::x_add(host::x_add(acc, a[0]), a[1]);
-    } else if (r >= p.logL && r - p.logL < p.logJ) {
-      acc = host::x_add(acc, a[2 + r - p.logL]);
-    }
+    if (r == 0) acc = host::x_add(host::x_add(acc, a[0]), a[1]);
+    // (the tree straight over the buckets has logL = 0: U_0 shares A's exponent)
+    if (r >= p.logL && r - p.logL < p.logJ) acc = host::x_add(acc, a[2 + r - p.logL]);
   }
   return acc;
 }
@@ -1524,10 +1583,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   add((size_t)p.J * p.W * sizeof(G1Xyzz) * 2);  // acc_j, T_j
   add(nfinal * sizeof(G1Xyzz));                 // group sums
   add(nfinal * gparts * sizeof(G1Xyzz));        // group slice sums
-  // running sums + subset-sum tree in one kernel (k_wsum_tree) when a window's segments fill whole
-  // 256-segment blocks (at most 64 per window); SVGPU_GROUP_TREE=0 keeps k_wsum + k_group_sum(_q)
-  bool group_tree = p.J % kTreeN == 0 && p.J / kTreeN <= 64;
-  if (const char* e = getenv("SVGPU_GROUP_TREE")) group_tree = group_tree && atoi(e) != 0;
+  const bool group_tree = p.tree != 0;  // see msm_plan
   const size_t ntree = group_tree ? (size_t)p.W * (p.J / kTreeN) * kTreeOut : 0;
   add(ntree * sizeof(G1Xyzz));                  // per-block tree outputs
   SV_TRY(ws->reserve(bytes));
@@ -1719,13 +1775,19 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   if (group_tree) {
     static thread_local int tree_attr_dev = -1;  // the > 64 KiB dynamic-LDS opt-in, once per thread/device
     if (tree_attr_dev != device) {
-      SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wsum_tree),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTreeLds));
+      SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wsum_tree<true>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)(2 * kTreeRow)));
       tree_attr_dev = device;
     }
-    hipLaunchKernelGGL(k_wsum_tree, dim3(p.J / kTreeN * p.W), dim3(kTreeN), kTreeLds, st, bsum,
-                       pieces > 1 ? nullptr : so[0].gst, p.B, p.J, 1u << p.logL, tree_out);
-    hipLaunchKernelGGL(k_group_fin, dim3(p.W * p.NG), dim3(64), 0, st, tree_out, p.J / kTreeN, p.NG, ping);
+    const uint32_t* gs = pieces > 1 ? nullptr : so[0].gst;
+    if (p.tree == 2)
+      hipLaunchKernelGGL(k_wsum_tree<false>, dim3(p.J / kTreeN * p.W), dim3(kTreeN), kTreeRow, st, bsum, gs, p.B,
+                         p.J, 1u, tree_out);
+    else
+      hipLaunchKernelGGL(k_wsum_tree<true>, dim3(p.J / kTreeN * p.W), dim3(kTreeN), 2 * kTreeRow, st, bsum, gs, p.B,
+                         p.J, 1u << p.logL, tree_out);
+    hipLaunchKernelGGL(k_group_fin, dim3(p.W * p.NG), dim3(128), 0, st, tree_out, p.J / kTreeN, p.NG,
+                       p.tree == 2 ? 1u : 0u, ping);
   } else {
     hipLaunchKernelGGL(k_wsum, dim3(cdiv((uint64_t)p.J * p.W, kBlock)), dim3(kBlock), 0, st, bsum,
                        pieces > 1 ? nullptr : so[0].gst, p.B, p.J, 1u << p.logL, p.W, 1, racc, rtot);

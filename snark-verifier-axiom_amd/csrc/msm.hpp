@@ -26,6 +26,7 @@ struct MsmPlan {
   bool glv;         // GLV split: 2n virtual points (P, phi(P)) with 128-bit scalar halves
   size_t npts;      // virtual points: n, or 2n with GLV
   int phi64;        // GLV table: whole phi(P) records (1) or beta x only (0)
+  int tree;         // bucket reduction: 0 k_wsum + k_group_sum, 1 running sums + tree, 2 tree over buckets
 };
 
 MsmPlan msm_plan(size_t n);

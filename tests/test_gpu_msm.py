@@ -233,18 +233,19 @@ def test_glv_phi_table_layouts(gpu, oracle_cpp, n, phi64, monkeypatch):
     assert svgpu.msm_arrays(B, S, svgpu.SV_CANONICAL) == exp
 
 
-@pytest.mark.parametrize("path", ["tree", "quad", "plain"])
+@pytest.mark.parametrize("path", ["tree", "bucket_tree", "quad", "plain"])
 @pytest.mark.parametrize("glv", ["0", "1"])
 def test_bucket_reduction_paths(gpu, oracle_cpp, monkeypatch, path, glv):
-    """The three bucket reductions -- running sums + in-block subset-sum tree (k_wsum_tree +
-    k_group_fin, the default once a window has >= 256 segments), and k_wsum with the quad-form or
-    whole-addition group sums -- give the reference Pippenger's point (msm.rs:238-316), on dense
+    """The four bucket reductions -- running sums + in-block subset-sum tree (k_wsum_tree<true> +
+    k_group_fin, the default once a window has >= 256 segments), the tree straight over the buckets
+    (k_wsum_tree<false>), and k_wsum with the quad-form or whole-addition group sums -- give the
+    reference Pippenger's point (msm.rs:238-316), on dense
     random scalars and on sparse ones whose windows leave most buckets / segments / tree blocks empty
     (identity partials at every tree level), device-resident and host-fed."""
     import svgpu
     from svgpu import encoding as enc
     monkeypatch.setenv("SVGPU_GLV", glv)
-    monkeypatch.setenv("SVGPU_GROUP_TREE", "1" if path == "tree" else "0")
+    monkeypatch.setenv("SVGPU_GROUP_TREE", {"tree": "1", "bucket_tree": "2"}.get(path, "0"))
     monkeypatch.setenv("SVGPU_GROUP_QUAD", "0" if path == "plain" else "1")
     for n, start in ((1 << 16, 5), (70001, 9)):
         B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=start)

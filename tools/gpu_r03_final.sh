@@ -19,5 +19,5 @@ run prof/trace_extras 600 rocprofv3 --kernel-trace --stats --output-format csv -
 run prof/pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --config4-log-n 0
 run prof/pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof/pmc_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --config4-log-n 0
 run prof/pmc_calib 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof/pmc_calib -o run -- ./tools/calib_fetch
-python3 tools/summarize_profile.py gpurun_out/prof gpurun_out/prof r03 > gpurun_out/prof/summary.log 2>&1 || { tail -5 gpurun_out/prof/summary.log; exit 1; }
+python3 tools/summarize_profile.py gpurun_out/prof gpurun_out/prof r03_final > gpurun_out/prof/summary.log 2>&1 || { tail -5 gpurun_out/prof/summary.log; exit 1; }
 tail -3 gpurun_out/prof/summary.log

@@ -88,13 +88,28 @@ def decide(g2, s_g2, lhs: torch.Tensor, rhs: torch.Tensor, form: int = _lib.SV_C
     ff = ctypes.c_int32(-2)
     verdicts = (ctypes.c_int32 * n)()
     gt = (_lib.sv_fq12 * n)() if want_gt else None
-    g2s, sg2s = enc.g2_struct(g2, form), enc.g2_struct(s_g2, form)
+    g2s, sg2s = _g2_struct_cached(g2, form), _g2_struct_cached(s_g2, form)
     _lib.check(_lib.lib.sv_bn254_kzg_decide_device(
         ctypes.byref(g2s), ctypes.byref(sg2s), lhs.data_ptr(), rhs.data_ptr(), n, form, d,
         _stream_handle(lhs.device), ctypes.byref(ff), ctypes.cast(verdicts, ctypes.c_void_p),
         ctypes.cast(gt, ctypes.c_void_p) if gt is not None else None), "sv_bn254_kzg_decide_device")
     gts = [enc.fq12_from_struct(g) for g in gt] if gt is not None else None
     return ff.value, list(verdicts), gts
+
+
+_G2_CACHE: dict = {}
+
+
+def _g2_struct_cached(q, form: int):
+    """A deciding key's G2 point as its ABI struct, converted once per key (a verifier decides with
+    one key over and over; the library only reads the struct during the call)."""
+    key = (q, form)
+    s = _G2_CACHE.get(key)
+    if s is None:
+        if len(_G2_CACHE) >= 16:
+            _G2_CACHE.clear()
+        s = _G2_CACHE[key] = enc.g2_struct(q, form)
+    return s
 
 
 def last_decide_kernel_ms() -> float:

@@ -268,9 +268,18 @@ __global__ void k_check_bases(const G1Aff* __restrict__ bases, uint32_t n, uint3
 // (window, bin) counting-sorts its ~n / NBIN entries by fine index inside that bin's region (L2
 // resident), writes ent[], the global bucket offsets gst[] and the owner bucket tstart[t] of every
 // accumulate chunk [tK, tK + K).  No per-(window, point) digit array is ever stored.
-// points per block in passes 1 and 3: 512 (2 per thread), 256 when the LDS staging of W digits
-// per point would not fit (small c, many windows)
-__host__ __device__ constexpr uint32_t sort_chunk(int ep) { return ep > 20 ? 256u : 512u; }  // ep: entries per point
+// points per block in passes 1 and 3: sort_chunk (below), 256 when the LDS staging of W digits per
+// point would not fit (small c, many windows)
+// Points per block of the histogram / scatter passes (ep: entries per point).  1024 (round 3) halves
+// the block count, so each (window, bin) run a scatter block writes is ~16 entries (64 B) instead of
+// ~8: sort 0.221 -> 0.206 ms at 2^20.  LDS: the scatter stages CH * ep u32 entries (2048 spilled
+// the scatter's digit registers: 336 B scratch, one wave per SIMD).
+#ifndef SV_SORT_CHUNK
+#define SV_SORT_CHUNK 1024
+#endif
+__host__ __device__ constexpr uint32_t sort_chunk(int ep) {
+  return ep > 20 ? 256u : (ep > 16 && SV_SORT_CHUNK > 1024 ? 1024u : (uint32_t)SV_SORT_CHUNK);
+}
 // coarse bits: 2^CB bins per window, so that W * 2^CB ~ 1024 fine-sort regions of ~16K entries at
 // 2^20 (LDS-staged in k_fine_sort) -- 64 bins for the 16 full-width windows, 128 for the 8 GLV ones
 __host__ __device__ constexpr int coarse_bits(int c, int nb) { return c - 1 < (nb == 128 ? 7 : 6) ? c - 1 : (nb == 128 ? 7 : 6); }
@@ -426,8 +435,9 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
   using D = Digits<C, GLV>;
   constexpr int W = D::W, LOGB = C - 1;
   constexpr int CB = coarse_bits(C, D::NB), FB = LOGB - CB, NBIN = 1 << CB, NK = W * NBIN;
-  // staged entry: local point (9 bits) | half << 9 | sign << 10 | fine << 11 | (window, bin) key << (11 + FB)
-  static_assert(11 + FB + ceil_log2(NK) <= 32, "staged entry overflows 32 bits");
+  // staged entry: local point (LP bits) | half << LP | sign << (LP + 1) | fine << (LP + 2) | (window, bin) key << (LP + 2 + FB)
+  constexpr int LP = ceil_log2((int)sort_chunk(D::EP));
+  static_assert(LP + 2 + FB + ceil_log2(NK) <= 32, "staged entry overflows 32 bits");
   constexpr uint32_t FMASK = (1u << FB) - 1;
   constexpr uint32_t CH = sort_chunk(D::EP), PT = CH / kBlock;
   __shared__ uint32_t off[NK];   // local group offsets
@@ -458,7 +468,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
           const uint32_t b = mag - 1;
           const uint32_t k = w * NBIN + (b >> FB);
           const uint32_t pos = atomicAdd(&cur[k], 1u);
-          stage[pos] = li | (half << 9) | (neg << 10) | ((b & FMASK) << 11) | (k << (11 + FB));
+          stage[pos] = li | (half << LP) | (neg << (LP + 1)) | ((b & FMASK) << (LP + 2)) | (k << (LP + 2 + FB));
         }
       });
     }
@@ -469,8 +479,8 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
   __syncthreads();
   for (uint32_t x = threadIdx.x; x < total; x += kBlock) {
     const uint32_t e = stage[x];
-    const uint32_t pt = lo + (e & 511u) + (((e >> 9) & 1u) ? n : 0u);
-    const uint32_t dst = cur[e >> (11 + FB)] + x, fine = (e >> 11) & FMASK, neg = (e >> 10) & 1u;
+    const uint32_t pt = lo + (e & ((1u << LP) - 1u)) + (((e >> LP) & 1u) ? n : 0u);
+    const uint32_t dst = cur[e >> (LP + 2 + FB)] + x, fine = (e >> (LP + 2)) & FMASK, neg = (e >> (LP + 1)) & 1u;
     if (e32) reinterpret_cast<uint32_t*>(tmp)[dst] = pack_entry32(fine, neg, pt, FB);
     else tmp[dst] = ((uint64_t)fine << 32) | pt | (neg << 31);
   }

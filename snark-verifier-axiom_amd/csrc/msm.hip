@@ -6,25 +6,27 @@
 //
 // Pipeline (all on one stream, inputs already in HBM):
 //   k_to_mont_bases   (canonical input only) bases -> Montgomery workspace copy
-//   k_bin_hist        per block of 2048 points: signed c-bit digits of every window (never
-//                     stored), LDS histogram of (window, coarse bin = top bits of the bucket)
+//   k_bin_hist        per block of sort_chunk points (1024 at 2^20): signed c-bit digits of every
+//                     window (never stored; GLV halves split on the fly) + the phi(P) table, LDS
+//                     histogram of (window, coarse bin = top bits of the bucket)
 //   k_bin_scan_chunks / k_bin_scan   offsets of every (window, bin, block) run
 //   k_bin_scatter     digits again; entries appended to their block's (window, bin) run -> tmp
-//   k_fine_sort       one block per (window, bin): counting sort by the fine bucket index inside
-//                     the bin's L2-resident region -> ent[], bucket offsets gst[], owner bucket of
-//                     every accumulate chunk tstart[]
+//   k_fine_sort<2>    one block per (window, bin), both region kinds in one launch: counting sort
+//                     by the fine bucket index inside the bin's L2-resident region -> ent[], bucket
+//                     offsets gst[], owner bucket of every accumulate chunk tstart[]
 //   k_accumulate      each thread sums K consecutive sorted entries (mixed XYZZ adds; perfect
 //                     load balance whatever the digit distribution), complete buckets written
 //                     directly, bucket pieces that cross a thread boundary to pfirst/plast
 //                     (two-piece buckets inside a block are joined at the end through LDS)
 //   k_fixup           the other crossing buckets, queued by k_accumulate (heavy ones: block-level
 //                     tree for buckets spanning more than 9 threads)
-//   k_wsum            bucket reduction, step 1: F_w = sum_b (b+1) S_b = sum_j acc_j + L sum_j j T_j
-//                     with running sums over segments of L = 8 buckets (acc_j, T_j per segment)
-//   k_group_sum       step 2: sum_j j T_j = sum_k 2^k U_k, U_k = sum_{j : bit k of j} T_j; the
-//                     subset sums U_k and the plain sum of acc_j are independent, so each is one
-//                     block-level tree reduction in LDS (low serial depth: the tail is latency-bound)
-//   host              Horner over (window, bit) terms (~255 doublings) -> affine, see host_ec.hpp
+//   k_wsum_tree       bucket reduction: F_w = sum_b (b+1) S_b = sum_j acc_j + L sum_j j T_j with
+//                     running sums over segments of L buckets (acc_j, T_j), then sum_j j T_j =
+//                     sum_k 2^k U_k, U_k = sum_{j : bit k of j} T_j, as a subset-sum tree over each
+//                     block's 256 segments in LDS (round 3; k_wsum + k_group_sum(_q) below for
+//                     windows of fewer than 256 segments)
+//   k_group_fin       the blocks' partial sums -> A and U_k per window
+//   host              ONE Horner over every (window, bit) exponent -> affine, see host_ec.hpp
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -439,6 +439,58 @@ __device__ __forceinline__ void merge_products(Fq2* __restrict__ M, const Fq2* _
   }
 }
 
+// Round 3 (k_decide_wg): the pair products D_idx from per-key constants.  With A = (c0 y1, c3 x1, c4)
+// and B = (c0' y2, c3' x2, c4') the line values at the accumulator's points, every coefficient of
+// D = A B is a sum of (product of two line coefficients: the key's) x (product of point coordinates:
+// the accumulator's) --
+//   d0 = (c0 c0') y1 y2 + xi c4 c4',  d1 = (c0 c3') y1 x2 + (c3 c0') x1 y2,  d2 = (c3 c3') x1 x2,
+//   d3 = (c0 c4') y1 + (c4 c0') y2,    d4 = (c3 c4') x1 + (c4 c3') x2,        d5 = 0
+// -- so the nine key products per step (kKc, computed once per deciding key on the host) leave one
+// fused two-product sum per Fq component: 880 independent jobs over the block instead of the line
+// evaluation (4 products per line) and a 6-product Karatsuba per pair (18 Fq products deep).
+// Identity points keep eval_lines + pair_products (the neutral line is not of this form).
+constexpr int kKc = 9;  // c0c0', c3c3', xi c4c4', c0c3', c3c0', c0c4', c4c0', c3c4', c4c3'
+__device__ __forceinline__ void pair_products_kc(Fq2* __restrict__ D, const Fq2* __restrict__ kc, const Fq* sc,
+                                                 const G1Aff& p1, const G1Aff& p2, int t, int nt) {
+  // sc: y1 y2, x1 x2, y1 x2, x1 y2 (LDS)
+  for (int job = t; job < ATE_NUM_LINES * 10; job += nt) {
+    const int idx = job / 10, r = job % 10, k = r >> 1, comp = r & 1;
+    const Fq2* K = kc + kKc * idx;
+    const int ja = k == 0 ? 0 : (k == 1 ? 3 : (k == 2 ? 1 : (k == 3 ? 5 : 7)));
+    const Fq2 ka = K[ja];
+    const Fq2 kb = K[k == 1 ? 4 : (k == 3 ? 6 : (k == 4 ? 8 : 2))];  // second term (k = 0: xi c4c4')
+    const bool two = k == 1 || k >= 3;
+    const Fq sa = k == 0 ? sc[0] : (k == 1 ? sc[2] : (k == 2 ? sc[1] : (k == 3 ? p1.y : p1.x)));
+    const Fq sb = k == 1 ? sc[3] : (k == 3 ? p2.y : p2.x);
+    const Fq x[2] = {comp ? ka.c1 : ka.c0, two ? (comp ? kb.c1 : kb.c0) : Fq::zero()};
+    const Fq y[2] = {sa, two ? sb : Fq::zero()};
+    Fq v = fe_mul_sum(x, y);
+    if (k == 0) v = v + (comp ? kb.c1 : kb.c0);
+    Fq2& d = D[6 * idx + k];
+    if (comp) d.c1 = v;
+    else d.c0 = v;
+  }
+  for (int idx = t; idx < ATE_NUM_LINES; idx += nt) D[6 * idx + 5] = Fq2::zero();
+}
+
+// the nine key products of kKc per step (host, once per deciding key): lines L1 (g2), L2 (-s_g2)
+static void pair_constants(const LineCoeff* L1, const LineCoeff* L2, Fq2* kc) {
+  for (int i = 0; i < ATE_NUM_LINES; i++) {
+    const LineCoeff& a = L1[i];
+    const LineCoeff& b = L2[i];
+    Fq2* K = kc + kKc * i;
+    K[0] = a.c0 * b.c0;
+    K[1] = a.c3 * b.c3;
+    K[2] = fq2_mul_xi(a.c4 * b.c4);
+    K[3] = a.c0 * b.c3;
+    K[4] = a.c3 * b.c0;
+    K[5] = a.c0 * b.c4;
+    K[6] = a.c4 * b.c0;
+    K[7] = a.c3 * b.c4;
+    K[8] = a.c4 * b.c3;
+  }
+}
+
 template <int S>
 __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ lhs, const G1Aff* __restrict__ rhs,
                                                       uint32_t n, const LineCoeff* __restrict__ L1,
@@ -1013,7 +1065,8 @@ constexpr size_t kLds = kLdsE + kLdsD + kLdsSlots + kLdsGamma;
 __global__ void __launch_bounds__(wg::kThreads) k_decide_wg(const G1Aff* __restrict__ lhs, const G1Aff* __restrict__ rhs,
                                                           uint32_t n, const LineCoeff* __restrict__ L1,
                                                           const LineCoeff* __restrict__ L2, int mont_in,
-                                                          int32_t* __restrict__ verdict, Fq12* __restrict__ gt) {
+                                                          int32_t* __restrict__ verdict, Fq12* __restrict__ gt,
+                                                          const Fq2* __restrict__ kc) {
   using namespace wg;
   extern __shared__ __attribute__((aligned(16))) unsigned char dec_lds[];
   __shared__ Fq2 tj[3], di;
@@ -1026,12 +1079,20 @@ __global__ void __launch_bounds__(wg::kThreads) k_decide_wg(const G1Aff* __restr
   for (int i = t; i < (int)(kLdsGamma / 4); i += kThreads) reinterpret_cast<uint32_t*>(gam)[i] = c_gamma[i];
   const uint32_t acc = blockIdx.x;
   G1Aff p1 = load_aff_d(lhs, acc, mont_in), p2 = load_aff_d(rhs, acc, mont_in);
-  // prologue: lines at the accumulator's points, pair products D, merged step multipliers M
-  eval_lines(E, L1, L2, p1, p2, t, kThreads);
+  // prologue: pair products D (from the key's constants; identity points evaluate the lines), merged
+  // step multipliers M
+  if (kc && !p1.is_identity() && !p2.is_identity()) {  // block-uniform
+    __shared__ Fq sc[4];
+    if (t < 4) sc[t] = (t == 1 || t == 3 ? p1.x : p1.y) * (t == 0 ? p2.y : (t == 3 ? p2.y : p2.x));
+    __syncthreads();
+    pair_products_kc(D, kc, sc, p1, p2, t, kThreads);
+  } else {
+    eval_lines(E, L1, L2, p1, p2, t, kThreads);
+    __syncthreads();
+    pair_products(D, E, t, kThreads);
+  }
   __syncthreads();
-  pair_products(D, E, t, kThreads);
-  __syncthreads();
-  merge_products(M, D, t, kThreads);
+  merge_products(M, D, t, kThreads);  // (a divergence-free 5-term walk measured no faster)
   __syncthreads();
   auto opnd = [&](uint16_t o) -> Fq2* {
     const uint32_t i = o & (kOpD - 1);
@@ -1080,12 +1141,14 @@ struct LineEntry {
   unsigned char key[2 * sizeof(G2Aff)];
   int device = 0;
   LineCoeff* d_lines = nullptr;  // 2 * ATE_NUM_LINES, written once before the entry is published
+  Fq2* d_kc = nullptr;           // kKc * ATE_NUM_LINES pair constants (k_decide_wg), same lifetime
   ~LineEntry() {
-    if (d_lines) {
+    if (d_lines || d_kc) {
       int prev = 0;
       (void)hipGetDevice(&prev);
       (void)hipSetDevice(device);
-      (void)hipFree(d_lines);
+      if (d_lines) (void)hipFree(d_lines);
+      if (d_kc) (void)hipFree(d_kc);
       (void)hipSetDevice(prev);
     }
   }
@@ -1154,8 +1217,12 @@ static int decider_lines(const sv_g2_affine* g2, const sv_g2_affine* s_g2, int f
   std::vector<LineCoeff> h(2 * ATE_NUM_LINES);
   g2_prepare(q1, h.data());
   g2_prepare(q2, h.data() + ATE_NUM_LINES);
+  std::vector<Fq2> kc((size_t)kKc * ATE_NUM_LINES);
+  pair_constants(h.data(), h.data() + ATE_NUM_LINES, kc.data());
   SV_HIP(hipMalloc(&ent->d_lines, h.size() * sizeof(LineCoeff)));
+  SV_HIP(hipMalloc(&ent->d_kc, kc.size() * sizeof(Fq2)));
   SV_HIP(hipMemcpyAsync(ent->d_lines, h.data(), h.size() * sizeof(LineCoeff), hipMemcpyHostToDevice, st));
+  SV_HIP(hipMemcpyAsync(ent->d_kc, kc.data(), kc.size() * sizeof(Fq2), hipMemcpyHostToDevice, st));
   SV_HIP(hipStreamSynchronize(st));
   {
     std::lock_guard<std::mutex> lk(c.mu);
@@ -1202,6 +1269,8 @@ int decide_run_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const vo
     cu_dev = device;
   }
   const int lanes = lanes_env ? lanes_env : (n <= (size_t)cus ? 256 : 48);
+  // k_decide_wg's pair products from the key's constants (SVGPU_DECIDER_KC=0: evaluate the lines)
+  static const bool kc_env = !getenv("SVGPU_DECIDER_KC") || atoi(getenv("SVGPU_DECIDER_KC")) != 0;
   static const int phases = getenv("SVGPU_DECIDER_PHASES") ? atoi(getenv("SVGPU_DECIDER_PHASES")) : 3;
   const G1Aff* dl = reinterpret_cast<const G1Aff*>(d_lhs);
   const G1Aff* dr = reinterpret_cast<const G1Aff*>(d_rhs);
@@ -1215,7 +1284,7 @@ int decide_run_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const vo
   }
   if (lanes == 256)
     hipLaunchKernelGGL(k_decide_wg, dim3((unsigned)n), dim3(wg::kThreads), wg::kLds, st, dl, dr, (uint32_t)n, lines,
-                       L2, mont, d_verdict, d_gt);
+                       L2, mont, d_verdict, d_gt, kc_env ? line_ref->d_kc : nullptr);
   else if (lanes == 48)
     hipLaunchKernelGGL(k_decide_lanes<8>, dim3((unsigned)n), dim3(64), 0, st, dl, dr, (uint32_t)n, lines, L2, mont,
                        d_verdict, d_gt, phases);

@@ -211,7 +211,9 @@ def cpu_baseline(args, n, gpu_result, g2, sg2, accs, enc):
         "cpu_model": cpu_model(),
         "host_cpus_visible": os.cpu_count(),
         "affinity_cores": aff_cores,
-        "threads_note": "cores = min(affinity cores, OMP_NUM_THREADS share of this GPU's box slice)",
+        "threads_note": "cores = min(affinity cores, OMP_NUM_THREADS share of this GPU's box slice); "
+                        "value_affinity_cores runs one thread per affinity core, which the box's cgroup CPU "
+                        "quota (cpu.max 1600000/100000 = 16 CPUs) throttles below the 16-thread value",
         "value_affinity_cores": n / aff_s if aff_s else n / cpu_s,
         "seconds": cpu_s,
         "parity_vs_gpu": bool(parity and cff == -1 and aff == -1 and c5ff == -1),

@@ -262,3 +262,10 @@ def test_bucket_reduction_paths(gpu, oracle_cpp, monkeypatch, path, glv):
     assert svgpu.msm_arrays(B, S) == _to_pt(oracle_cpp.msm_pippenger(B, S, 0)), "sparse"
     monkeypatch.setenv("SVGPU_H2D_PIECES", "3")
     assert svgpu.msm_arrays(B, S) == _to_pt(oracle_cpp.msm_pippenger(B, S, 0)), "sparse host-fed"
+    if path == "bucket_tree" and glv == "1":
+        # c = 16: 128 tree blocks per window, so k_group_fin sums U_k (k < 8) over two waves
+        monkeypatch.delenv("SVGPU_H2D_PIECES")
+        n = 1 << 19
+        B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=23)
+        S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=23)
+        assert svgpu.msm_arrays(B, S) == _to_pt(oracle_cpp.msm_pippenger(B, S, 0)), "2^19"

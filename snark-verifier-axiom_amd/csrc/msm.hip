@@ -6,7 +6,7 @@
 //
 // Pipeline (all on one stream, inputs already in HBM):
 //   k_to_mont_bases   (canonical input only) bases -> Montgomery workspace copy
-//   k_bin_hist        per block of sort_chunk points (1024 at 2^20): signed c-bit digits of every
+//   k_bin_hist        per block of sort_chunk points (1024 at 2^20; XCD-aware block map, sort_block): signed c-bit digits of every
 //                     window (never stored; GLV halves split on the fly) + the phi(P) table, LDS
 //                     histogram of (window, coarse bin = top bits of the bucket)
 //   k_bin_scan_chunks / k_bin_scan   offsets of every (window, bin, block) run
@@ -334,12 +334,24 @@ __device__ __forceinline__ uint64_t load_entry(const uint64_t* __restrict__ tmp,
   return ((uint64_t)fine << 32) | pt | (neg << 31);
 }
 
+// Logical block of the histogram / scatter passes.  Workgroups are dispatched round-robin over the
+// 8 XCDs, so consecutive blocks sit on different L2s; both passes store per-block counts column-wise
+// (bcnt[key * nblk + blk], 32 blocks per 128-B line) and runs of consecutive blocks side by side in
+// tmp, and a line filled from 8 L2s is written back 8 times, partially.  xcd != 0 gives each XCD a
+// contiguous range of logical blocks instead (a bijection; the tail n % 8 blocks keep their index).
+__device__ __forceinline__ uint32_t sort_block(uint32_t b, uint32_t n, int xcd) {
+  const uint32_t nfull = n & ~7u;
+  if (!xcd || b >= nfull) return b;
+  return (b & 7u) * (nfull >> 3) + (b >> 3);
+}
+
 // With GLV the pass also writes the beta-x table of its points (phix, see glv_phix).
 template <int C, bool GLV>
 __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scalars, uint32_t n, int mont_in,
                                                      uint32_t nblk, uint32_t* __restrict__ bcnt,
                                                      uint32_t* __restrict__ err, const G1Aff* __restrict__ bases,
-                                                     uint4* __restrict__ phix, int phi64, int check_bases) {
+                                                     uint4* __restrict__ phix, int phi64, int check_bases,
+                                                     int xcd) {
   using D = Digits<C, GLV>;
   constexpr int W = D::W, LOGB = C - 1;
   constexpr int CB = coarse_bits(C, D::NB), FB = LOGB - CB, NBIN = 1 << CB;
@@ -347,7 +359,8 @@ __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scal
   for (int k = threadIdx.x; k < W * NBIN; k += kBlock) h[k] = 0;
   __syncthreads();
   constexpr uint32_t CH = sort_chunk(D::EP);
-  const uint32_t lo = blockIdx.x * CH, hi = min(n, lo + CH);
+  const uint32_t blk = sort_block(blockIdx.x, gridDim.x, xcd);
+  const uint32_t lo = blk * CH, hi = min(n, lo + CH);
   for (uint32_t i = lo + threadIdx.x; i < hi; i += kBlock) {
     // Montgomery bases are checked here (canonical ones by k_to_mont_bases)
     if constexpr (GLV) {
@@ -366,7 +379,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scal
   }
   __syncthreads();
   // layout bcnt[(w * NBIN + bin) * nblk + blk]: each (window, bin) scans over contiguous blocks
-  for (int k = threadIdx.x; k < W * NBIN; k += kBlock) bcnt[(size_t)k * nblk + blockIdx.x] = h[k];
+  for (int k = threadIdx.x; k < W * NBIN; k += kBlock) bcnt[(size_t)k * nblk + blk] = h[k];
 }
 
 // one 256-thread block per (window, bin): exclusive scan over blocks in place, total -> btot
@@ -433,7 +446,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
                                                         uint32_t nblk, const uint32_t* __restrict__ bcnt,
                                                         const uint32_t* __restrict__ btot,
                                                         const uint32_t* __restrict__ bstart,
-                                                        uint64_t* __restrict__ tmp, int e32) {
+                                                        uint64_t* __restrict__ tmp, int e32, int xcd) {
   using D = Digits<C, GLV>;
   constexpr int W = D::W, LOGB = C - 1;
   constexpr int CB = coarse_bits(C, D::NB), FB = LOGB - CB, NBIN = 1 << CB, NK = W * NBIN;
@@ -446,7 +459,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
   __shared__ uint32_t cur[NK];   // cursors
   __shared__ uint32_t part[kBlock];
   __shared__ uint32_t stage[CH * D::EP];  // see the layout above (no separate key array: 3 blocks per CU)
-  const uint32_t blk = blockIdx.x, lo = blk * CH, hi = min(n, lo + CH);
+  const uint32_t blk = sort_block(blockIdx.x, gridDim.x, xcd), lo = blk * CH, hi = min(n, lo + CH);
   for (int k = threadIdx.x; k < NK; k += kBlock) {
     const size_t at = (size_t)k * nblk + blk;
     off[k] = (blk + 1 < nblk ? bcnt[at + 1] : btot[k]) - bcnt[at];
@@ -1398,8 +1411,9 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
   const uint64_t vmax = p.glv ? (uint64_t)nsplit + npts : (uint64_t)npts;
   int e32 = vmax <= (uint64_t(1) << (31 - FB)) ? 1 : 0;
   if (const char* e = getenv("SVGPU_SORT_E32")) e32 = e32 && atoi(e) != 0;
+  static const int xcd = !getenv("SVGPU_SORT_XCD") || atoi(getenv("SVGPU_SORT_XCD")) != 0 ? 1 : 0;
   SV_LAUNCH_C(k_bin_hist, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.err, bases,
-              phix, p.phi64, check_bases);
+              phix, p.phi64, check_bases, xcd);
   SV_HIP(hipGetLastError());
   if (ev_sort_mid) SV_HIP(hipEventRecord(ev_sort_mid, st));
   hipLaunchKernelGGL(k_bin_scan_chunks, dim3(nwb), dim3(kBlock), 0, st, w.bcnt, nblk, w.btot);
@@ -1407,7 +1421,7 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
   // measured 12 -> 122 us for that kernel: the fence writes back the XCD's L2)
   hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, w.btot, nwb, w.bstart, so.gst + p.nbt);
   SV_LAUNCH_C(k_bin_scatter, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.btot, w.bstart,
-              w.tmp, e32);
+              w.tmp, e32, xcd);
   static thread_local int fine_attr_dev = -1;  // the > 64 KiB dynamic-LDS opt-in, once per thread/device
   if (fine_attr_dev != device) {
     SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort<0>),

@@ -351,7 +351,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scal
                                                      uint32_t nblk, uint32_t* __restrict__ bcnt,
                                                      uint32_t* __restrict__ err, const G1Aff* __restrict__ bases,
                                                      uint4* __restrict__ phix, int phi64, int check_bases,
-                                                     int xcd) {
+                                                     int xcd, int bm) {
   using D = Digits<C, GLV>;
   constexpr int W = D::W, LOGB = C - 1;
   constexpr int CB = coarse_bits(C, D::NB), FB = LOGB - CB, NBIN = 1 << CB;
@@ -378,8 +378,10 @@ __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scal
     });
   }
   __syncthreads();
-  // layout bcnt[(w * NBIN + bin) * nblk + blk]: each (window, bin) scans over contiguous blocks
-  for (int k = threadIdx.x; k < W * NBIN; k += kBlock) bcnt[(size_t)k * nblk + blk] = h[k];
+  // bm: block-major bcnt[blk * NK + (w * NBIN + bin)], one contiguous 4-KB row per block (the scan
+  // reads it in 32-key tiles); else key-major bcnt[(w * NBIN + bin) * nblk + blk] (round 2)
+  for (int k = threadIdx.x; k < W * NBIN; k += kBlock)
+    bcnt[bm ? (size_t)blk * (W * NBIN) + k : (size_t)k * nblk + blk] = h[k];
 }
 
 // one 256-thread block per (window, bin): exclusive scan over blocks in place, total -> btot
@@ -406,6 +408,44 @@ __global__ void __launch_bounds__(kBlock) k_bin_scan_chunks(uint32_t* __restrict
     run += v;
   }
   if (tid == kBlock - 1) btot[blockIdx.x] = part[kBlock - 1];
+}
+
+// Block-major counts (bcnt[blk * nk + key]): one 1024-thread block per 32 keys.  Thread (grp, kk)
+// walks rows grp * per .. of key 32 tile + kk, so each row access of a wave reads or writes two whole
+// 128-B lines; exclusive scan over blocks in place, total -> btot.
+__global__ void __launch_bounds__(1024) k_bin_scan_tiles(uint32_t* __restrict__ bcnt, uint32_t nblk, uint32_t nk,
+                                                         uint32_t* __restrict__ btot) {
+  __shared__ uint32_t part[32][33];
+  const uint32_t kk = threadIdx.x & 31, grp = threadIdx.x >> 5, key = blockIdx.x * 32 + kk;
+  const uint32_t per = (nblk + 31) / 32, lo = min(nblk, grp * per), hi = min(nblk, lo + per);
+  const bool live = key < nk;
+  uint32_t* c = bcnt + key;
+  uint32_t sum = 0;
+  if (live) {
+#pragma unroll 8
+    for (uint32_t b = lo; b < hi; b++) sum += c[(size_t)b * nk];
+  }
+  part[grp][kk] = sum;
+  __syncthreads();
+  if (threadIdx.x < 32) {  // per key: exclusive scan over the 32 row groups
+    uint32_t run = 0;
+    for (int g = 0; g < 32; g++) {
+      const uint32_t v = part[g][threadIdx.x];
+      part[g][threadIdx.x] = run;
+      run += v;
+    }
+    if (blockIdx.x * 32 + threadIdx.x < nk) btot[blockIdx.x * 32 + threadIdx.x] = run;
+  }
+  __syncthreads();
+  if (live) {
+    uint32_t run = part[grp][kk];
+#pragma unroll 8
+    for (uint32_t b = lo; b < hi; b++) {
+      const uint32_t v = c[(size_t)b * nk];
+      c[(size_t)b * nk] = run;
+      run += v;
+    }
+  }
 }
 
 // one 1024-thread block: exclusive scan of btot over all (window, bin) -> bstart; bstart[nwb] = total
@@ -446,7 +486,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
                                                         uint32_t nblk, const uint32_t* __restrict__ bcnt,
                                                         const uint32_t* __restrict__ btot,
                                                         const uint32_t* __restrict__ bstart,
-                                                        uint64_t* __restrict__ tmp, int e32, int xcd) {
+                                                        uint64_t* __restrict__ tmp, int e32, int xcd, int bm) {
   using D = Digits<C, GLV>;
   constexpr int W = D::W, LOGB = C - 1;
   constexpr int CB = coarse_bits(C, D::NB), FB = LOGB - CB, NBIN = 1 << CB, NK = W * NBIN;
@@ -461,8 +501,8 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
   __shared__ uint32_t stage[CH * D::EP];  // see the layout above (no separate key array: 3 blocks per CU)
   const uint32_t blk = sort_block(blockIdx.x, gridDim.x, xcd), lo = blk * CH, hi = min(n, lo + CH);
   for (int k = threadIdx.x; k < NK; k += kBlock) {
-    const size_t at = (size_t)k * nblk + blk;
-    off[k] = (blk + 1 < nblk ? bcnt[at + 1] : btot[k]) - bcnt[at];
+    const size_t at = bm ? (size_t)blk * NK + k : (size_t)k * nblk + blk;
+    off[k] = (blk + 1 < nblk ? bcnt[bm ? at + NK : at + 1] : btot[k]) - bcnt[at];
   }
   D dg[PT];
 #pragma unroll
@@ -490,7 +530,8 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
   }
   __syncthreads();
   // global position of local slot x = gbase[key] + x  (cur[] reused for gbase)
-  for (int k = threadIdx.x; k < NK; k += kBlock) cur[k] = bstart[k] + bcnt[(size_t)k * nblk + blk] - off[k];
+  for (int k = threadIdx.x; k < NK; k += kBlock)
+    cur[k] = bstart[k] + bcnt[bm ? (size_t)blk * NK + k : (size_t)k * nblk + blk] - off[k];
   __syncthreads();
   for (uint32_t x = threadIdx.x; x < total; x += kBlock) {
     const uint32_t e = stage[x];
@@ -1412,16 +1453,21 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
   int e32 = vmax <= (uint64_t(1) << (31 - FB)) ? 1 : 0;
   if (const char* e = getenv("SVGPU_SORT_E32")) e32 = e32 && atoi(e) != 0;
   static const int xcd = !getenv("SVGPU_SORT_XCD") || atoi(getenv("SVGPU_SORT_XCD")) != 0 ? 1 : 0;
+  // block-major per-block counts + the tiled scan (SVGPU_SORT_BM=0: key-major, k_bin_scan_chunks)
+  static const int bm = !getenv("SVGPU_SORT_BM") || atoi(getenv("SVGPU_SORT_BM")) != 0 ? 1 : 0;
   SV_LAUNCH_C(k_bin_hist, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.err, bases,
-              phix, p.phi64, check_bases, xcd);
+              phix, p.phi64, check_bases, xcd, bm);
   SV_HIP(hipGetLastError());
   if (ev_sort_mid) SV_HIP(hipEventRecord(ev_sort_mid, st));
-  hipLaunchKernelGGL(k_bin_scan_chunks, dim3(nwb), dim3(kBlock), 0, st, w.bcnt, nblk, w.btot);
+  if (bm)
+    hipLaunchKernelGGL(k_bin_scan_tiles, dim3(cdiv(nwb, 32)), dim3(1024), 0, st, w.bcnt, nblk, nwb, w.btot);
+  else
+    hipLaunchKernelGGL(k_bin_scan_chunks, dim3(nwb), dim3(kBlock), 0, st, w.bcnt, nblk, w.btot);
   // (fusing this scan into k_bin_scan_chunks' last block -- device-scope fence + counter -- was
   // measured 12 -> 122 us for that kernel: the fence writes back the XCD's L2)
   hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, w.btot, nwb, w.bstart, so.gst + p.nbt);
   SV_LAUNCH_C(k_bin_scatter, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.btot, w.bstart,
-              w.tmp, e32, xcd);
+              w.tmp, e32, xcd, bm);
   static thread_local int fine_attr_dev = -1;  // the > 64 KiB dynamic-LDS opt-in, once per thread/device
   if (fine_attr_dev != device) {
     SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort<0>),

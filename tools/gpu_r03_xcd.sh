@@ -3,11 +3,11 @@
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof
-bash tools/gpu_r03_iter.sh "test_gpu_msm or host_path or threads" "SVGPU_SORT_XCD=0" "SVGPU_SORT_XCD=1" "SVGPU_SORT_XCD=0" "SVGPU_SORT_XCD=1" "SVGPU_SORT_XCD=0" "SVGPU_SORT_XCD=1" || exit $?
-for x in 0 1; do
-  SVGPU_SORT_XCD=$x timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof/xcd_write$x -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --config4-log-n 0 > gpurun_out/prof/xcd_write$x.log 2>&1
+bash tools/gpu_r03_iter.sh "test_gpu_msm or host_path or threads" "$@" || exit $?
+for x in ${PMC_SET:-0 1}; do
+  env ${PMC_VAR:-SVGPU_SORT_XCD}=$x timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof/xcd_write$x -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --config4-log-n 0 > gpurun_out/prof/xcd_write$x.log 2>&1
   rc=$?; echo "[pmc write xcd=$x] rc=$rc"; [ $rc -ne 0 ] && exit $rc
-  SVGPU_SORT_XCD=$x timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof/xcd_fetch$x -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --config4-log-n 0 > gpurun_out/prof/xcd_fetch$x.log 2>&1
+  env ${PMC_VAR:-SVGPU_SORT_XCD}=$x timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof/xcd_fetch$x -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --config4-log-n 0 > gpurun_out/prof/xcd_fetch$x.log 2>&1
   rc=$?; echo "[pmc fetch xcd=$x] rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
 python3 - <<'EOF'
@@ -18,7 +18,7 @@ for tag in ("write0", "write1", "fetch0", "fetch1"):
     for f in fs:
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
-            for key in ("k_bin_hist", "k_bin_scatter", "k_bin_scan_chunks", "k_fine_sort", "k_accumulate"):
+            for key in ("k_bin_hist", "k_bin_scatter", "k_bin_scan_chunks", "k_bin_scan_tiles", "k_fine_sort", "k_accumulate"):
                 if key in k:
                     acc[key].append(float(r["Counter_Value"]))
     print(tag, {k: round(sum(v) / len(v)) for k, v in acc.items()})

@@ -12,6 +12,8 @@
 #![allow(clippy::missing_safety_doc)]
 
 use halo2curves::bn256::{Fq, Fr, G1Affine, G2Affine};
+use halo2curves::pairing::Engine;
+use halo2curves::CurveAffine;
 use std::os::raw::{c_char, c_int, c_void};
 use std::sync::OnceLock;
 
@@ -210,6 +212,67 @@ pub fn cast_back<C: 'static + Copy>(p: G1Affine) -> C {
 
 fn g1_out(p: SvG1Affine) -> G1Affine {
     unsafe { std::mem::transmute::<SvG1Affine, G1Affine>(p) }
+}
+
+fn same_type<A: 'static, B: 'static>() -> bool {
+    std::any::TypeId::of::<A>() == std::any::TypeId::of::<B>()
+}
+
+/// True when the pairing engine `M` is halo2curves' BN254 (`bn256::Bn256`): its G1 and G2 affine
+/// types are `bn256::G1Affine` / `bn256::G2Affine`.  Needs no `M: 'static` bound (the decider's
+/// `impl<M: MultiMillerLoop, MOS>` has none, pcs/kzg/decider.rs:53-57): the engine's affine types
+/// are `PrimeCurveAffine`, which is `'static`.
+pub fn is_bn256<M: Engine>() -> bool {
+    same_type::<M::G1Affine, G1Affine>() && same_type::<M::G2Affine, G2Affine>()
+}
+
+/// `Some(&[bn256::G1Affine])` view of a generic curve's slice when `C` is `bn256::G1Affine`.
+pub fn as_g1_slice<C: 'static>(points: &[C]) -> Option<&[G1Affine]> {
+    // SAFETY: C == G1Affine (checked): same type, same length, same lifetime
+    same_type::<C, G1Affine>()
+        .then(|| unsafe { std::slice::from_raw_parts(points.as_ptr() as *const G1Affine, points.len()) })
+}
+
+/// `Some(&bn256::G2Affine)` view of a generic G2 point when `G` is `bn256::G2Affine`.
+pub fn as_g2<G: 'static>(point: &G) -> Option<&G2Affine> {
+    // SAFETY: G == G2Affine (checked)
+    same_type::<G, G2Affine>().then(|| unsafe { &*(point as *const G as *const G2Affine) })
+}
+
+/// NativeLoader::multi_scalar_multiplication for a generic curve (loader/native.rs:61-71): the
+/// call site passes its `&[(&C::Scalar, &C)]` unchanged.  `None` when `C` is not BN254 G1 (or its
+/// scalar not `bn256::Fr`), when no GPU is usable, or on a device error; the caller then runs its
+/// own CPU fold.  The `SvMsmRef`s are built straight from the generic pairs, so nothing is cast
+/// unless both `TypeId`s match.  Panics on empty input like the reference (native.rs:69).
+pub fn msm_generic<C: CurveAffine>(pairs: &[(&C::Scalar, &C)]) -> Option<C> {
+    if pairs.is_empty() {
+        panic!("pairs should not be empty");
+    }
+    if !(same_type::<C, G1Affine>() && same_type::<C::Scalar, Fr>()) || !available() {
+        return None;
+    }
+    let refs: Vec<SvMsmRef> = pairs
+        .iter()
+        .map(|(s, b)| SvMsmRef { scalar: *s as *const C::Scalar as *const SvFe, base: *b as *const C as *const SvG1Affine })
+        .collect();
+    let mut out = SvG1Affine::default();
+    let rc = unsafe { sv_bn254_g1_msm_refs(refs.as_ptr(), refs.len(), SV_MONTGOMERY, 0, &mut out) };
+    (rc == SV_OK).then(|| cast_back::<C>(g1_out(out)))
+}
+
+/// decide_all for a generic engine's points (pcs/kzg/decider.rs:70-80): `dk.g2`, `dk.s_g2` and the
+/// accumulators' `lhs`/`rhs` as the decider holds them (`M::G2Affine`, `M::G1Affine`).
+/// `Some(-1)` = all pass, `Some(i)` = first failing accumulator (`try_collect` order), `None` =
+/// not BN254, no GPU, or a device error (the caller keeps its sequential CPU decide).
+pub fn decide_all_generic<G1: 'static, G2: 'static>(g2: &G2, s_g2: &G2, lhs: &[G1], rhs: &[G1]) -> Option<i32> {
+    assert!(!lhs.is_empty());
+    assert_eq!(lhs.len(), rhs.len());
+    let (g2, s_g2) = (as_g2(g2)?, as_g2(s_g2)?);
+    let (lhs, rhs) = (as_g1_slice(lhs)?, as_g1_slice(rhs)?);
+    if !available() {
+        return None;
+    }
+    decide_all(g2, s_g2, lhs, rhs)
 }
 
 /// NativeLoader::multi_scalar_multiplication (snark-verifier/src/loader/native.rs:61-71): the

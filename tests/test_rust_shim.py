@@ -81,3 +81,45 @@ def test_msm_slices_panics_on_empty_like_the_reference():
     ref = open("/root/reference/snark-verifier/src/util/msm.rs").read() if os.path.exists("/root/reference") else None
     if ref is not None:
         assert "let num_bytes = scalars[0].as_ref().len();" in ref
+
+
+def _crate_exports(rs):
+    """Public items of the crate: fns (generic or not), structs, consts."""
+    out = set(re.findall(r"\bpub (?:unsafe )?fn ([a-z_][a-z0-9_]*)\s*[<(]", rs))
+    out |= set(re.findall(r"\bpub struct ([A-Za-z0-9_]+)", rs))
+    out |= set(re.findall(r"\bpub const ([A-Z0-9_]+)", rs))
+    return out
+
+
+def test_integration_call_sites_use_exported_items():
+    """Every `snark_verifier_gpu::X` that INTEGRATION.md's call sites name exists in lib.rs, and the
+    three hot-path sites (native.rs:61-71, msm.rs:287-316, decider.rs:70-80) each go through it."""
+    rs = open(os.path.join(ROOT, "snark-verifier-gpu", "src", "lib.rs")).read()
+    md = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    exports = _crate_exports(rs)
+    used = set(re.findall(r"snark_verifier_gpu::([A-Za-z_][A-Za-z0-9_]*)", md))
+    assert {"msm_generic", "cast_slices", "msm_slices", "cast_back", "is_bn256", "decide_all_generic"} <= used
+    missing = used - exports
+    assert not missing, f"INTEGRATION.md names items lib.rs does not export: {sorted(missing)}"
+    # no helper is called unqualified at the call sites unless the crate exports it
+    sites = md[md.index("## 2."):md.index("## 3.")]
+    code = "\n".join(re.findall(r"```rust\n(.*?)```", sites, flags=re.S))
+    for name in ("unsafe_cast_pairs", "gpu_min_msm", "cast(&"):
+        assert name not in code, name
+    for site in ("loader/native.rs:61-71", "util/msm.rs:287-316", "pcs/kzg/decider.rs:70-80"):
+        assert site in code, site
+
+
+def test_generic_helpers_check_types_before_casting():
+    """msm_generic / as_g1_slice / as_g2 are safe fns: each compares TypeIds before reinterpreting."""
+    rs = open(os.path.join(ROOT, "snark-verifier-gpu", "src", "lib.rs")).read()
+    body = _fn_body(rs, "msm_generic")
+    assert "same_type::<C, G1Affine>()" in body and "same_type::<C::Scalar, Fr>()" in body
+    assert body.index("same_type::<C, G1Affine>()") < body.index("unsafe {")
+    assert 'panic!("pairs should not be empty")' in body
+    for fn, check in (("as_g1_slice", "same_type::<C, G1Affine>()"), ("as_g2", "same_type::<G, G2Affine>()")):
+        b = _fn_body(rs, fn) if "\n}\n" in rs[rs.index("pub fn " + fn):] else ""
+        assert check in b, fn
+    body = _fn_body(rs, "is_bn256")
+    assert "M::G1Affine" in body and "M::G2Affine" in body
+    assert re.search(r"pub fn is_bn256<M: Engine>\(\)", rs)

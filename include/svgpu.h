@@ -10,6 +10,7 @@
  *   sv_bn254_kzg_decide      replaces  AccumulationDecider::{decide, decide_all} for KzgAs on NativeLoader
  *                                      snark-verifier/src/pcs/kzg/decider.rs:60-68 and :70-80
  *   sv_bn254_kzg_accumulate  replaces  KzgAs::create_proof's two MSMs (no zk blind)
+ *   sv_bn254_kzg_create_proof   the same with r squeezed from the Poseidon transcript
  *                                      snark-verifier/src/pcs/kzg/accumulation.rs:146-195
  *                                      (also AccumulationScheme::verify, :40-62)
  *
@@ -117,6 +118,20 @@ int sv_bn254_kzg_decide_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2,
 int sv_bn254_kzg_accumulate(const sv_g1_affine* lhs, const sv_g1_affine* rhs, size_t n,
                             const sv_fe* r, int form, int num_gpus, sv_g1_affine* out_lhs,
                             sv_g1_affine* out_rhs) SV_NOEXCEPT;
+
+/* KzgAs::create_proof without blind, challenge included (accumulation.rs:146-195): a fresh
+ * Poseidon transcript (T = 3, RATE = 2, R_F = 8, R_P = 57, snark-verifier-sdk/src/halo2.rs:52-55)
+ * absorbs lhs[i], rhs[i] for i = 0..n through common_ec_point (x, y as Fq -> Fr mod r,
+ * system/halo2/transcript/halo2.rs:214-226), squeezes r (accumulation.rs:176), then returns the
+ * sv_bn254_kzg_accumulate result for that r.  sponge_state (3 elements in `form`, may be
+ * NULL = a fresh transcript, Poseidon::new's (2^64, 0, 0)) is the transcript's sponge state before
+ * the call and receives it after the squeeze, for a transcript that was squeezed before (its
+ * buffer empty).  out_r (may be NULL) receives r in `form`.  An identity accumulator point is
+ * SV_ERR_ARG (the reference's Error::Transcript, halo2.rs:215-223).  The sponge (n + 1 dependent
+ * permutations) runs on the host; the MSMs on the device.                                    */
+int sv_bn254_kzg_create_proof(const sv_g1_affine* lhs, const sv_g1_affine* rhs, size_t n, int form,
+                              int num_gpus, sv_g1_affine* out_lhs, sv_g1_affine* out_rhs,
+                              sv_fe* sponge_state, sv_fe* out_r) SV_NOEXCEPT;
 
 /* ---- batched small MSMs -------------------------------------
  * count independent MSMs over shared arrays: MSM k = sum_{i in [offsets[k], offsets[k+1])}

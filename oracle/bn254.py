@@ -875,6 +875,21 @@ def accumulate(accumulators: Sequence[Tuple], r: int):
     return lhs, rhs
 
 
+def create_proof(accumulators: Sequence[Tuple], state: Optional[Sequence[int]] = None):
+    """KzgAs::create_proof without blind (snark-verifier/src/pcs/kzg/accumulation.rs:146-195):
+    a Poseidon transcript (fresh, or continuing from sponge `state`) absorbs every lhs_i, rhs_i via
+    common_ec_point (system/halo2/transcript/halo2.rs:214-226: x, y as Fq -> Fr by fe_to_fe, i.e.
+    mod r; the identity has no coordinates -> Error::Transcript), squeezes r (:176), then the two
+    r^i MSMs.  Returns ((lhs, rhs), r, the sponge state after the squeeze)."""
+    from . import poseidon as op
+    sponge = op.Sponge(3, state)
+    for a in accumulators:
+        op.transcript_common_ec_point(sponge, a[0])
+        op.transcript_common_ec_point(sponge, a[1])
+    r = sponge.squeeze()
+    return accumulate(accumulators, r), r, list(sponge.state)
+
+
 def fe_to_limbs(x: int, limbs: int = 3, bits: int = 88) -> List[int]:
     mask = (1 << bits) - 1
     return [(x >> (bits * i)) & mask for i in range(limbs)]

@@ -19,6 +19,7 @@
 #include "decider.hpp"
 #include "gen.hpp"
 #include "host_ec.hpp"
+#include "host_poseidon.hpp"
 #include "msm.hpp"
 #include "msm_batch.hpp"
 #include "poseidon.hpp"
@@ -466,6 +467,75 @@ int sv_bn254_kzg_accumulate(const sv_g1_affine* lhs, const sv_g1_affine* rhs, si
   const Xyzz& b = ab[1];
   affine_out(a, form, out_lhs);
   affine_out(b, form, out_rhs);
+  return SV_OK;
+  SV_GUARD_END
+}
+
+// KzgAs::create_proof without blind (accumulation.rs:146-195): a fresh PoseidonTranscript
+// (T = 3, RATE = 2, R_F = 8, R_P = 57; snark-verifier-sdk/src/halo2.rs:52-55) absorbs every lhs_i,
+// rhs_i through common_ec_point (transcript/halo2.rs:214-226: the affine x and y, each Fq -> Fr by
+// fe_to_fe = reduction mod r) and squeezes r (:158-176); then the two r^i MSMs.  The sponge is one
+// serial chain of n + 1 permutations and runs on the host (host_poseidon.hpp: a GPU lane would
+// take ~20 ms for it at n = 64); the MSMs run on the device (sv_bn254_kzg_accumulate).
+int sv_bn254_kzg_create_proof(const sv_g1_affine* lhs, const sv_g1_affine* rhs, size_t n, int form, int num_gpus,
+                              sv_g1_affine* out_lhs, sv_g1_affine* out_rhs, sv_fe* sponge_state,
+                              sv_fe* out_r) noexcept {
+  SV_GUARD_BEGIN
+  if (n == 0) {
+    sv::set_error("accumulators should not be empty");
+    return SV_ERR_EMPTY;
+  }
+  if (!lhs || !rhs || !out_lhs || !out_rhs) {
+    sv::set_error("null pointer");
+    return SV_ERR_ARG;
+  }
+  SV_TRY(check_form(form));
+  namespace fr = sv::host::fr;
+  fr::Sponge3 sponge;
+  if (sponge_state) {
+    for (int k = 0; k < 3; k++) {
+      fr::E e;
+      memcpy(e.l, sponge_state[k].l, 32);
+      if (!fr::is_reduced(e)) {
+        sv::set_error("sponge_state[%d] not reduced mod r", k);
+        return SV_ERR_ARG;
+      }
+      sponge.st[k] = form == SV_MONTGOMERY ? e : fr::to_mont(e);
+    }
+  }
+  sponge.buf.reserve(4 * n);
+  for (size_t i = 0; i < n; i++) {
+    for (const sv_g1_affine* pt : {&lhs[i], &rhs[i]}) {
+      F x = fe_in(pt->x), y = fe_in(pt->y);
+      if (host::f_is_zero(x) && host::f_is_zero(y)) {
+        // coordinates() of the identity is None -> Error::Transcript (halo2.rs:215-223)
+        sv::set_error("Invalid elliptic curve point encoding in proof (accumulator %zu is the identity)", i);
+        return SV_ERR_ARG;
+      }
+      if (!host::f_is_reduced(x) || !host::f_is_reduced(y)) {
+        sv::set_error("accumulator %zu: coordinate not reduced mod p", i);
+        return SV_ERR_ARG;
+      }
+      if (form == SV_MONTGOMERY) x = host::f_from_mont(x), y = host::f_from_mont(y);
+      for (const F& c : {x, y}) {
+        fr::E e;
+        memcpy(e.l, c.l, 32);
+        sponge.update(fr::to_mont(fr::reduce_below_2r(e)));  // fe_to_fe: canonical Fq mod r
+      }
+    }
+  }
+  const fr::E rm = sponge.squeeze();
+  const fr::E rv = form == SV_MONTGOMERY ? rm : fr::from_mont(rm);
+  sv_fe r;
+  memcpy(r.l, rv.l, 32);
+  const int rc = sv_bn254_kzg_accumulate(lhs, rhs, n, &r, form, num_gpus, out_lhs, out_rhs);
+  if (rc != SV_OK) return rc;
+  if (out_r) *out_r = r;
+  if (sponge_state)
+    for (int k = 0; k < 3; k++) {
+      const fr::E e = form == SV_MONTGOMERY ? sponge.st[k] : fr::from_mont(sponge.st[k]);
+      memcpy(sponge_state[k].l, e.l, 32);
+    }
   return SV_OK;
   SV_GUARD_END
 }

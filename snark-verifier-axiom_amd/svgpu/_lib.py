@@ -98,6 +98,8 @@ PROTOTYPES = [
                                             c_size_t, c_int, c_int, c_void_p, POINTER(c_int32), c_void_p, c_void_p]),
     ("sv_bn254_kzg_accumulate", c_int, [c_void_p, c_void_p, c_size_t, POINTER(sv_fe), c_int, c_int,
                                          POINTER(sv_g1_affine), POINTER(sv_g1_affine)]),
+    ("sv_bn254_kzg_create_proof", c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, POINTER(sv_g1_affine),
+                                           POINTER(sv_g1_affine), c_void_p, c_void_p]),
     ("sv_bn254_g1_msm_batch", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
     ("sv_bn254_g1_msm_batch_device", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_int, c_int,
                                               c_void_p, c_void_p]),

@@ -7,7 +7,14 @@
 * ``KzgAs.create_proof`` / ``KzgAs.verify`` mirror the accumulation MSMs of
   snark-verifier/src/pcs/kzg/accumulation.rs:146-195 / :40-62 without the zk blind:
   lhs = sum r^i lhs_i, rhs = sum r^i rhs_i with r^0 = 1 (snark-verifier/src/loader.rs:71-78).
-  The challenge ``r`` is an input: deriving it from the Poseidon transcript is outside the path.
+  ``create_proof(instances, transcript)`` is the reference's own signature: the accumulators' lhs
+  and rhs are absorbed through ``transcript.common_ec_point`` and r is squeezed from it
+  (accumulation.rs:156-176).  Given a fresh ``PoseidonTranscript`` (what the SDK passes,
+  snark-verifier-sdk/src/halo2/aggregation.rs:235-242) the whole call is ONE library call,
+  ``sv_bn254_kzg_create_proof`` (host sponge, device MSMs); a used transcript's sponge state goes
+  in and comes back out of the same call, and one with buffered input is absorbed and squeezed
+  through ``svgpu.poseidon`` first.  An ``int`` in place of the
+  transcript is taken as r itself (``sv_bn254_kzg_accumulate``).
 """
 from __future__ import annotations
 
@@ -85,9 +92,43 @@ class KzgAs:
         return decide_arrays(dk, lhs, rhs, _lib.SV_CANONICAL, num_gpus)
 
     @staticmethod
-    def create_proof(instances: Sequence[KzgAccumulator], r: int) -> KzgAccumulator:
+    def create_proof(instances: Sequence[KzgAccumulator], transcript=None) -> KzgAccumulator:
+        """KzgAs::create_proof with the default proving key (no blind), accumulation.rs:146-195.
+
+        ``transcript``: None or a fresh ``PoseidonTranscript`` -> r from the library's transcript
+        (one call); a used ``PoseidonTranscript`` -> absorbed / squeezed through it; an int -> r."""
         if len(instances) == 0:
             raise ReferencePanic("assertion failed: !instances.is_empty()")
+        from .poseidon import PoseidonTranscript
+        if isinstance(transcript, int):
+            return KzgAs._accumulate(instances, transcript)
+        if transcript is not None and (not isinstance(transcript, PoseidonTranscript) or transcript.buf.buf
+                                       or transcript.buf.t != 3):
+            # a transcript with pending input (or another kind): absorb and squeeze through it
+            for a in instances:
+                transcript.common_ec_point(a.lhs)
+                transcript.common_ec_point(a.rhs)
+            return KzgAs._accumulate(instances, transcript.squeeze_challenge())
+        lhs = enc.bases_array([a.lhs for a in instances])
+        rhs = enc.bases_array([a.rhs for a in instances])
+        out_l, out_r = _lib.sv_g1_affine(), _lib.sv_g1_affine()
+        r = np.zeros(4, dtype=np.uint64)
+        state = None
+        if transcript is not None:  # continue from the transcript's sponge state, then hand it back
+            state = enc.ints_to_limbs([int(v) for v in transcript.buf.state])
+        _lib.check(_lib.lib.sv_bn254_kzg_create_proof(lhs.ctypes.data, rhs.ctypes.data, len(instances),
+                                                      _lib.SV_CANONICAL, 0, ctypes.byref(out_l), ctypes.byref(out_r),
+                                                      None if state is None else state.ctypes.data, r.ctypes.data),
+                   "sv_bn254_kzg_create_proof")
+        if transcript is not None:
+            transcript.buf.state = [enc.limbs_to_int(row) for row in state]
+        KzgAs.last_challenge = enc.limbs_to_int(r)
+        return KzgAccumulator(enc.g1_from_struct(out_l), enc.g1_from_struct(out_r))
+
+    last_challenge: Optional[int] = None
+
+    @staticmethod
+    def _accumulate(instances: Sequence[KzgAccumulator], r: int) -> KzgAccumulator:
         if not 0 <= r < enc.R:
             raise ValueError("r must be a reduced Fr element")
         lhs = enc.bases_array([a.lhs for a in instances])
@@ -97,6 +138,11 @@ class KzgAs:
         _lib.check(_lib.lib.sv_bn254_kzg_accumulate(lhs.ctypes.data, rhs.ctypes.data, len(instances),
                                                     ctypes.byref(rr), _lib.SV_CANONICAL, 0, ctypes.byref(out_l),
                                                     ctypes.byref(out_r)), "sv_bn254_kzg_accumulate")
+        KzgAs.last_challenge = r
         return KzgAccumulator(enc.g1_from_struct(out_l), enc.g1_from_struct(out_r))
 
-    verify = create_proof  # AccumulationScheme::verify computes the same two MSMs (accumulation.rs:40-62)
+    @staticmethod
+    def verify(instances: Sequence[KzgAccumulator], transcript=None) -> KzgAccumulator:
+        """AccumulationScheme::verify (accumulation.rs:40-62): the same transcript and MSMs."""
+        return KzgAs.create_proof(instances, transcript)
+

@@ -109,6 +109,9 @@ extern "C" {
     pub fn sv_bn254_kzg_accumulate(lhs: *const SvG1Affine, rhs: *const SvG1Affine, n: usize, r: *const SvFe,
                                    form: c_int, num_gpus: c_int, out_lhs: *mut SvG1Affine,
                                    out_rhs: *mut SvG1Affine) -> c_int;
+    pub fn sv_bn254_kzg_create_proof(lhs: *const SvG1Affine, rhs: *const SvG1Affine, n: usize, form: c_int,
+                                     num_gpus: c_int, out_lhs: *mut SvG1Affine, out_rhs: *mut SvG1Affine,
+                                     sponge_state: *mut SvFe, out_r: *mut SvFe) -> c_int;
     pub fn sv_bn254_g1_msm_batch(bases: *const SvG1Affine, scalars: *const SvFe, offsets: *const u64,
                                  count: usize, form: c_int, out: *mut SvG1Affine) -> c_int;
     pub fn sv_bn254_g1_msm_batch_device(d_bases: *const SvG1Affine, d_scalars: *const SvFe, d_offsets: *const u64,
@@ -333,6 +336,29 @@ pub fn accumulate(lhs: &[G1Affine], rhs: &[G1Affine], r: &Fr) -> Option<(G1Affin
                                 r as *const Fr as *const SvFe, SV_MONTGOMERY, 0, &mut ol, &mut or)
     };
     (rc == SV_OK).then(|| (g1_out(ol), g1_out(or)))
+}
+
+/// KzgAs::create_proof without blind, challenge included (pcs/kzg/accumulation.rs:146-195): the
+/// accumulators are absorbed into a Poseidon transcript (fresh when `sponge_state` is None, else
+/// continuing from that state, which receives the state after the squeeze) and r is squeezed
+/// (:158-176); returns (Σ rⁱ lhsᵢ, Σ rⁱ rhsᵢ, r).  `Err(true)` = an identity accumulator point
+/// (the reference's Error::Transcript), `Err(false)` = device error.
+pub fn create_proof(lhs: &[G1Affine], rhs: &[G1Affine], sponge_state: Option<&mut [Fr; 3]>)
+                    -> Result<(G1Affine, G1Affine, Fr), bool> {
+    assert!(!lhs.is_empty());
+    assert_eq!(lhs.len(), rhs.len());
+    let (mut ol, mut or) = (SvG1Affine::default(), SvG1Affine::default());
+    let mut r = Fr::zero();
+    let st = sponge_state.map_or(std::ptr::null_mut(), |s| s.as_mut_ptr() as *mut SvFe);
+    let rc = unsafe {
+        sv_bn254_kzg_create_proof(lhs.as_ptr() as *const SvG1Affine, rhs.as_ptr() as *const SvG1Affine, lhs.len(),
+                                  SV_MONTGOMERY, 0, &mut ol, &mut or, st, &mut r as *mut Fr as *mut SvFe)
+    };
+    match rc {
+        SV_OK => Ok((g1_out(ol), g1_out(or), r)),
+        SV_ERR_ARG => Err(true),
+        _ => Err(false),
+    }
 }
 
 /// Many small MSMs in one launch: MSM k = terms offsets[k]..offsets[k+1].

@@ -91,8 +91,11 @@ def main():
     accum = {"r": hex(acc_r), "lhs": [hp(a[0]) for a in accs[:6]], "rhs": [hp(a[1]) for a in accs[:6]]}
     el, er = b.accumulate(accs[:6], acc_r)
     accum["expected"] = [hp(el), hp(er)]
-    json.dump({"cases": dec, "pairing": pair, "accumulate": accum}, open(os.path.join(OUT, "decider.json"), "w"),
-              indent=1)
+    # KzgAs::create_proof with the challenge from a fresh Poseidon transcript (accumulation.rs:156-176)
+    (cl, cr), cr_r, _ = b.create_proof(accs[:6])
+    cproof = {"lhs": accum["lhs"], "rhs": accum["rhs"], "r": hex(cr_r), "expected": [hp(cl), hp(cr)]}
+    json.dump({"cases": dec, "pairing": pair, "accumulate": accum, "create_proof": cproof},
+              open(os.path.join(OUT, "decider.json"), "w"), indent=1)
     # The reference's own known-answer vectors (snark-verifier/src/util/hash/poseidon/tests.rs:6-85)
     kat = {
         "source": "snark-verifier/src/util/hash/poseidon/tests.rs:6-85 (HADES poseidonperm_x5_254_3/_5)",

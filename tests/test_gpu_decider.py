@@ -118,3 +118,82 @@ def test_both_decider_kernels_gt_and_first_fail(gpu, oracle_cpp, monkeypatch, la
     assert sum(1 for v in verdicts if not v) == n // 20 + (1 if n % 20 > 13 else 0)
     for i in (0, 13, n - 3, n - 1):
         assert [int(x) for x in gts[i]] == [enc.limbs_to_int(egt[i][4 * c:4 * c + 4]) for c in range(12)], i
+
+
+def test_create_proof_transcript_golden(gpu, golden_decider):
+    """KzgAs::create_proof(instances, transcript) with a fresh Poseidon transcript
+    (accumulation.rs:146-195): r squeezed after absorbing every lhs_i, rhs_i (common_ec_point,
+    transcript/halo2.rs:214-226) equals the oracle's, and so do the two r^i MSMs."""
+    import svgpu
+    c = golden_decider["create_proof"]
+    accs = [svgpu.KzgAccumulator(pt(l), pt(r)) for l, r in zip(c["lhs"], c["rhs"])]
+    out = svgpu.KzgAs.create_proof(accs, svgpu.PoseidonTranscript())
+    assert svgpu.KzgAs.last_challenge == int(c["r"], 16)
+    assert [out.lhs, out.rhs] == [pt(c["expected"][0]), pt(c["expected"][1])]
+
+
+def test_config5_create_proof_64_transcript_vs_oracle(gpu):
+    """Config 5: 64 accumulators -> transcript-derived r -> accumulate -> decide, against the oracle;
+    also in Montgomery form through the C ABI (r and the outputs as Montgomery limbs)."""
+    import ctypes
+    import svgpu
+    from svgpu import _lib, encoding as enc
+    g2, sg2, accs = b.gen_decider_case(64, seed=0x64)
+    (el, er), r, state = b.create_proof(accs)
+    inst = [svgpu.KzgAccumulator(*x) for x in accs]
+    out = svgpu.KzgAs.create_proof(inst)
+    assert svgpu.KzgAs.last_challenge == r
+    assert (out.lhs, out.rhs) == (el, er)
+    svgpu.KzgAs.decide(svgpu.KzgDecidingKey(b.G1_GEN, g2, sg2), out)
+    # Montgomery form, with the sponge state handed back
+    M = svgpu.SV_MONTGOMERY
+    L = enc.bases_array([a[0] for a in accs], M)
+    R_ = enc.bases_array([a[1] for a in accs], M)
+    ol, orr = _lib.sv_g1_affine(), _lib.sv_g1_affine()
+    rr = np.zeros(4, np.uint64)
+    st = enc.ints_to_limbs([(1 << 64) * (1 << 256) % enc.R, 0, 0])  # fresh state, Montgomery
+    _lib.check(_lib.lib.sv_bn254_kzg_create_proof(L.ctypes.data, R_.ctypes.data, 64, M, 0, ctypes.byref(ol),
+                                                  ctypes.byref(orr), st.ctypes.data, rr.ctypes.data), "create_proof")
+    mont = lambda v: v * (1 << 256) % enc.R  # noqa: E731
+    assert enc.limbs_to_int(rr) == mont(r)
+    assert [enc.limbs_to_int(row) for row in st] == [mont(v) for v in state]
+    assert (enc.g1_from_struct(ol, M), enc.g1_from_struct(orr, M)) == (el, er)
+
+
+def test_create_proof_continues_a_used_transcript(gpu):
+    """A transcript squeezed before (empty buffer): its sponge state goes into the library call and
+    the state after the squeeze comes back, as the reference's transcript would hold it."""
+    import svgpu
+    g2, sg2, accs = b.gen_decider_case(5, seed=0x55)
+    tr = svgpu.PoseidonTranscript()
+    tr.common_scalar(12345)
+    c0 = tr.squeeze_challenge()
+    state0 = list(tr.buf.state)
+    out = svgpu.KzgAs.create_proof([svgpu.KzgAccumulator(*x) for x in accs], tr)
+    (el, er), r, state = b.create_proof(accs, state0)
+    assert c0 != r and svgpu.KzgAs.last_challenge == r
+    assert (out.lhs, out.rhs) == (el, er)
+    assert tr.buf.state == state
+    # a transcript with buffered input is absorbed and squeezed through svgpu.poseidon (device sponge)
+    tr2 = svgpu.PoseidonTranscript()
+    tr2.common_scalar(7)
+    out2 = svgpu.KzgAs.create_proof([svgpu.KzgAccumulator(*x) for x in accs], tr2)
+    from oracle import poseidon as op
+    sp = op.Sponge(3)
+    sp.update([7])
+    for a in accs:
+        op.transcript_common_ec_point(sp, a[0])
+        op.transcript_common_ec_point(sp, a[1])
+    r2 = sp.squeeze()
+    assert (out2.lhs, out2.rhs) == b.accumulate(accs, r2)
+
+
+def test_create_proof_rejects_identity_and_empty(gpu):
+    import svgpu
+    from svgpu.loader import ReferencePanic
+    g2, sg2, accs = b.gen_decider_case(3, seed=0x33)
+    inst = [svgpu.KzgAccumulator(*x) for x in accs] + [svgpu.KzgAccumulator(None, accs[0][1])]
+    with pytest.raises(svgpu.ArgumentError, match="Invalid elliptic curve point encoding"):
+        svgpu.KzgAs.create_proof(inst)
+    with pytest.raises(ReferencePanic):
+        svgpu.KzgAs.create_proof([])

@@ -25,14 +25,20 @@ namespace {
 // job g cannot complete before that slice's done_ increment, so the fields it reads are job g's.
 class HostPool {
  public:
-  static constexpr uint64_t kIdxBits = 20, kIdxMask = (uint64_t(1) << kIdxBits) - 1;
+  // slice count and next-slice index are at most kMaxThreads (parts <= nthreads_), so 11 bits each
+  // leave 42 bits of job generation: a wrap needs 2^42 jobs (~10^11 host-fed calls at ~12 jobs
+  // each), i.e. a straggler would have to stall across 4e12 jobs to see its generation again
+  static constexpr int kMaxThreads = 1024;
+  static constexpr uint64_t kIdxBits = 11, kIdxMask = (uint64_t(1) << kIdxBits) - 1;
+  static_assert((uint64_t(1) << kIdxBits) > (uint64_t)kMaxThreads, "slice index must hold nthreads_");
+  static_assert(64 - 2 * kIdxBits >= 40, "job generation needs >= 40 bits");
   using Fn = std::function<void(size_t, size_t)>;
 
   HostPool() {
     int hw = (int)std::thread::hardware_concurrency();
     nthreads_ = hw > 16 ? 16 : (hw > 0 ? hw : 1);
     if (const char* e = getenv("SVGPU_HOST_THREADS")) nthreads_ = atoi(e) > 0 ? atoi(e) : 1;
-    if (nthreads_ > 1024) nthreads_ = 1024;
+    if (nthreads_ > kMaxThreads) nthreads_ = kMaxThreads;
     for (int i = 1; i < nthreads_; i++) workers_.emplace_back([this] { loop(); });
     for (auto& w : workers_) w.detach();  // the pool lives for the process
   }

@@ -1766,14 +1766,24 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
     std::string feed_err;
     SV_TRY(ws->run_helper([&] {
       int rc = SV_OK;
-      for (int k = 0; k < pieces && !stop.load(std::memory_order_relaxed); k++) {
-        const size_t lo = pb[k], hi = pb[k + 1];
-        rc = feed->stage_scalars(lo, hi, const_cast<Fr*>(scalars) + lo, cs, ev[8 + 3 * k]);
-        if (rc != SV_OK) break;
-        staged.store(2 * k + 1, std::memory_order_release);
-        rc = feed->stage_bases(lo, hi, const_cast<G1Aff*>(bases) + lo, cs, ev[9 + 3 * k]);
-        if (rc != SV_OK) break;
-        staged.store(2 * k + 2, std::memory_order_release);
+      // the helper thread has no SV_GUARD: an exception here (std::function / vector allocation in
+      // the host pool) becomes the call's SV_ERR_DEVICE instead of std::terminate
+      try {
+        for (int k = 0; k < pieces && !stop.load(std::memory_order_relaxed); k++) {
+          const size_t lo = pb[k], hi = pb[k + 1];
+          rc = feed->stage_scalars(lo, hi, const_cast<Fr*>(scalars) + lo, cs, ev[8 + 3 * k]);
+          if (rc != SV_OK) break;
+          staged.store(2 * k + 1, std::memory_order_release);
+          rc = feed->stage_bases(lo, hi, const_cast<G1Aff*>(bases) + lo, cs, ev[9 + 3 * k]);
+          if (rc != SV_OK) break;
+          staged.store(2 * k + 2, std::memory_order_release);
+        }
+      } catch (const std::exception& e) {
+        set_error("host-fed MSM feeder: %s", e.what());
+        rc = SV_ERR_DEVICE;
+      } catch (...) {
+        set_error("host-fed MSM feeder: unknown exception");
+        rc = SV_ERR_DEVICE;
       }
       if (rc != SV_OK) {
         feed_rc = rc;

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 
@@ -476,11 +477,11 @@ __device__ __forceinline__ void bucket_window(BucketSmem& sm, uint32_t k, uint32
 
 // Bounded wait for a window's bucket sums (fused kernel): a wave that never sees the flag (a bug,
 // not a schedule: see k_batch_fused) raises error bit 8 and goes on, so the grid always drains
-__device__ __forceinline__ void wait_ready(const uint32_t* f, uint32_t* err) {
+__device__ __forceinline__ void wait_ready(const uint32_t* f, uint32_t* err, uint32_t spin_max) {
   uint32_t spins = 0;
   while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
     __builtin_amdgcn_s_sleep(8);
-    if (++spins > (1u << 22)) {
+    if (++spins > spin_max) {
       if (threadIdx.x == 0) atomicOr(err, 8u);
       break;
     }
@@ -494,15 +495,15 @@ __device__ __forceinline__ void wait_ready(const uint32_t* f, uint32_t* err) {
 template <bool kWait>
 __device__ __forceinline__ void horner_msm(uint32_t k, const G1Xyzz* __restrict__ Sb, const uint32_t* __restrict__ ids,
                                            int mont, G1Aff* __restrict__ out, const uint32_t* ready,
-                                           uint32_t* err) {
+                                           uint32_t* err, uint32_t spin_max) {
   const int c = threadIdx.x & 3, b = threadIdx.x >> 2;
   const uint32_t id = ids ? ids[k] : k;
   const G1Xyzz* S = Sb + ((size_t)k * kQB + b) * kQW;
-  if (kWait) wait_ready(ready + (size_t)k * kQW + kQW - 1, err);
+  if (kWait) wait_ready(ready + (size_t)k * kQW + kQW - 1, err, spin_max);
   Fq acc = quad::ld(S + kQW - 1, c);
 #pragma unroll 1
   for (int w = kQW - 2; w >= 0; w--) {
-    if (kWait) wait_ready(ready + (size_t)k * kQW + w, err);
+    if (kWait) wait_ready(ready + (size_t)k * kQW + w, err, spin_max);
     const Fq nxt = quad::ld(S + w, c);
 #pragma unroll 1
     for (int i = 0; i < kQC; i++) acc = quad::dbl_2p(acc, c);
@@ -541,7 +542,7 @@ __global__ void __launch_bounds__(64) k_batch_buckets_q(const uint64_t* __restri
 __global__ void __launch_bounds__(64) k_batch_horner_b(const G1Xyzz* __restrict__ Sb,
                                                        const uint32_t* __restrict__ ids, int mont,
                                                        G1Aff* __restrict__ out) {
-  horner_msm<false>(blockIdx.x, Sb, ids, mont, out, nullptr, nullptr);
+  horner_msm<false>(blockIdx.x, Sb, ids, mont, out, nullptr, nullptr, 0);
 }
 
 // Both in ONE launch, so the Horner (the batch's latency floor: ~475 dependent product levels) runs
@@ -558,11 +559,12 @@ __global__ void __launch_bounds__(64) k_batch_fused(const uint64_t* __restrict__
                                                     uint32_t count, uint32_t max_terms,
                                                     const uint8_t* __restrict__ dig, const G1Aff* __restrict__ pts,
                                                     G1Xyzz* __restrict__ Sb, uint32_t* ready, uint32_t* err,
-                                                    int mont, G1Aff* __restrict__ out, uint32_t bw) {
+                                                    int mont, G1Aff* __restrict__ out, uint32_t bw,
+                                                    uint32_t spin_max) {
   __shared__ BucketSmem sm;
   if (blockIdx.x < count) {
     __builtin_amdgcn_s_setprio(3);
-    horner_msm<true>(blockIdx.x, Sb, ids, mont, out, ready, err);
+    horner_msm<true>(blockIdx.x, Sb, ids, mont, out, ready, err, spin_max);
     return;
   }
   const uint32_t i = blockIdx.x - count;
@@ -902,6 +904,8 @@ __global__ void __launch_bounds__(kThreads) k_msm_batch_fixed(const G1Aff* __res
 
 }  // namespace
 
+static std::atomic<uint64_t> g_fused_redone{0};  // fused launches redone by the two-kernel path
+
 int msm_batch_window_bits(size_t max_terms) {
   if (const char* e = getenv("SVGPU_BATCH_WINDOW_BITS")) {
     const int c = atoi(e);
@@ -938,8 +942,30 @@ int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t*
   const size_t nT = bucket_horner ? count * kQB * kQW : count * W;
   // one launch for buckets + Horner while the Horner waves stay few (k_batch_fused; SVGPU_BATCH_FUSE=0
   // runs the two kernels back to back)
-  const bool fused = bucket_horner && count <= kFuseMax &&
-                     (!getenv("SVGPU_BATCH_FUSE") || atoi(getenv("SVGPU_BATCH_FUSE")) != 0);
+  // HIP promises no co-residency between workgroups of a launch, and the Horner waves of a fused
+  // launch hold their slots while they wait: one fused launch (count <= kFuseMax waves) leaves most
+  // of the chip's wave slots to its bucket blocks, but several at once on one GPU (concurrent
+  // callers, SVGPU_DEVICE_MAP repeats) could fill it with waiting waves.  So at most ONE fused launch
+  // is in flight per physical device; the others take the two-kernel path.  A launch whose wait
+  // times out anyway (error bit 8) is redone below by the two-kernel path, never reported.
+  bool fused = bucket_horner && count <= kFuseMax &&
+               (!getenv("SVGPU_BATCH_FUSE") || atoi(getenv("SVGPU_BATCH_FUSE")) != 0);
+  struct FuseSlot {
+    std::atomic<int>* slot = nullptr;
+    ~FuseSlot() {
+      if (slot) slot->fetch_sub(1, std::memory_order_acq_rel);
+    }
+  } fuse_slot;
+  if (fused) {
+    static std::atomic<int> inflight[64];
+    std::atomic<int>& f = inflight[device & 63];
+    if (f.fetch_add(1, std::memory_order_acq_rel) == 0) {
+      fuse_slot.slot = &f;
+    } else {
+      f.fetch_sub(1, std::memory_order_acq_rel);
+      fused = false;
+    }
+  }
   const size_t nflag = fused ? count * kQW : 0;
   SV_TRY(ws->reserve(Workspace::aligned(4 * (1 + nflag)) + Workspace::aligned(nT * sizeof(G1Xyzz)) +
                      Workspace::aligned(dig_bytes ? dig_bytes : 1) + Workspace::aligned(pts_bytes ? pts_bytes : 1)));
@@ -961,9 +987,13 @@ int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t*
                        dim3(kThreads), 0, st, b, s, d_offsets, d_ids, mont, (uint32_t)max_terms, dig, pts, err, d_bidx,
                        table_len, mont_b);
     if (fused) {
+      // SVGPU_BATCH_WAIT_SPINS: the wait bound (default 2^22 sleeps, ~1 s); tests set it to 0 to
+      // force the timeout and the two-kernel redo
+      const char* spins_env = getenv("SVGPU_BATCH_WAIT_SPINS");
+      const uint32_t spin_max = spins_env ? (uint32_t)strtoul(spins_env, nullptr, 10) : (1u << 22);
       const uint32_t bw = std::min<uint32_t>(kQW, std::max(1, getenv("SVGPU_BATCH_BW") ? atoi(getenv("SVGPU_BATCH_BW")) : 4));
       hipLaunchKernelGGL(k_batch_fused, dim3((uint32_t)(count * (1 + bw))), dim3(64), 0, st, d_offsets, d_ids,
-                         (uint32_t)count, (uint32_t)max_terms, dig, pts, Tg, err + 1, err, mont, o, bw);
+                         (uint32_t)count, (uint32_t)max_terms, dig, pts, Tg, err + 1, err, mont, o, bw, spin_max);
     } else if (bucket_horner) {
       hipLaunchKernelGGL(k_batch_buckets_q, dim3((uint32_t)count, (uint32_t)kQW), dim3(64), 0, st, d_offsets, d_ids,
                          (uint32_t)max_terms, dig, pts, Tg);
@@ -1009,11 +1039,20 @@ int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t*
     return SV_ERR_ARG;
   }
   if (ev & 8u) {
-    set_error("msm_batch: a Horner wave timed out waiting for its window sums");
-    return SV_ERR_DEVICE;
+    // a fused launch's Horner wave gave up waiting (the GPU was full of other waves): its outputs
+    // are garbage, so redo the bucket sums and the Horner as two ordered launches
+    SV_HIP(hipMemsetAsync(err, 0, 4, st));
+    hipLaunchKernelGGL(k_batch_buckets_q, dim3((uint32_t)count, (uint32_t)kQW), dim3(64), 0, st, d_offsets, d_ids,
+                       (uint32_t)max_terms, dig, pts, Tg);
+    hipLaunchKernelGGL(k_batch_horner_b, dim3((uint32_t)count), dim3(64), 0, st, Tg, d_ids, mont, o);
+    SV_HIP(hipGetLastError());
+    SV_HIP(hipStreamSynchronize(st));
+    g_fused_redone.fetch_add(1, std::memory_order_relaxed);
   }
   return SV_OK;
 }
+
+uint64_t msm_batch_fused_redone() { return g_fused_redone.load(std::memory_order_relaxed); }
 
 }  // namespace sv
 

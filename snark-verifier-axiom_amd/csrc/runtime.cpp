@@ -85,13 +85,14 @@ int Workspace::reserve_in(size_t bytes) {
 
 // Gather staging of sv_bn254_g1_msm_refs: pinned.  (Measured round 3 at 2^20, shuffled refs:
 // pinned 3.00 ms, pageable staging through the runtime's own copy path 5.4 ms, pinned non-coherent
-// 5.3 ms.)
+// 5.3 ms.)  The staging is read by DMAs queued on the copy stream of a DIFFERENT workspace (the
+// MSM's, leased in msm_run_impl), so this workspace's streams say nothing about them.  The
+// invariant that makes freeing / reusing it safe: msm_run_fed drains its copy stream before it
+// returns (its Drain guard, on every exit path), and api.cpp releases the staging lease only after
+// msm_run_fed has returned -- so no DMA can read a staging buffer once its lease is back in the pool.
 int Workspace::reserve_stage(size_t bytes) {
   if (bytes <= stage_cap) return SV_OK;
-  if (stage) {
-    SV_TRY(quiesce());  // the copy stream may still be reading the staging
-    SV_HIP(hipHostFree(stage));
-  }
+  if (stage) SV_HIP(hipHostFree(stage));
   stage = nullptr;
   stage_cap = 0;
   SV_HIP(hipHostMalloc(&stage, bytes, hipHostMallocDefault));
@@ -116,27 +117,38 @@ struct Workspace::Helper {
 
 int Workspace::run_helper(std::function<void()> job) {
   if (!helper) {
-    helper = new Helper();
-    Helper* h = helper;
+    // `helper` is published only once its thread runs: if the thread cannot be created, no later
+    // call queues a job that nothing would ever run (msm_run_impl's wait_stage would spin forever)
+    Helper* h = new Helper();
     const int dev = device;
-    std::thread([h, dev] {
-      (void)hipSetDevice(dev);
-      for (;;) {
-        std::function<void()> j;
-        {
-          std::unique_lock<std::mutex> lk(h->mu);
-          h->cv.wait(lk, [h] { return h->pending; });
-          j = std::move(h->job);
-          h->pending = false;
+    try {
+      std::thread([h, dev] {
+        (void)hipSetDevice(dev);
+        for (;;) {
+          std::function<void()> j;
+          {
+            std::unique_lock<std::mutex> lk(h->mu);
+            h->cv.wait(lk, [h] { return h->pending; });
+            j = std::move(h->job);
+            h->pending = false;
+          }
+          try {
+            j();  // jobs report their own failures; nothing may escape the thread
+          } catch (...) {
+          }
+          {
+            std::lock_guard<std::mutex> lk(h->mu);
+            h->busy = false;
+          }
+          h->cv.notify_all();
         }
-        j();
-        {
-          std::lock_guard<std::mutex> lk(h->mu);
-          h->busy = false;
-        }
-        h->cv.notify_all();
-      }
-    }).detach();  // lives with the pooled workspace, for the process
+      }).detach();  // lives with the pooled workspace, for the process
+    } catch (const std::exception& e) {
+      delete h;
+      set_error("workspace helper thread: %s", e.what());
+      return SV_ERR_DEVICE;
+    }
+    helper = h;
   }
   {
     std::lock_guard<std::mutex> lk(helper->mu);

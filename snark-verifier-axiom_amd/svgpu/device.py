@@ -100,10 +100,19 @@ def decide(g2, s_g2, lhs: torch.Tensor, rhs: torch.Tensor, form: int = _lib.SV_C
 _G2_CACHE: dict = {}
 
 
+def _frozen(v):
+    """Nested lists (a G2 point as ((x0, x1), (y0, y1)) in any sequence type) as nested tuples."""
+    return tuple(_frozen(x) for x in v) if isinstance(v, (list, tuple)) else v
+
+
 def _g2_struct_cached(q, form: int):
     """A deciding key's G2 point as its ABI struct, converted once per key (a verifier decides with
     one key over and over; the library only reads the struct during the call)."""
-    key = (q, form)
+    try:
+        key = (_frozen(q), form)
+        hash(key)
+    except TypeError:  # something hash cannot take even after freezing: no caching
+        return enc.g2_struct(q, form)
     s = _G2_CACHE.get(key)
     if s is None:
         if len(_G2_CACHE) >= 16:

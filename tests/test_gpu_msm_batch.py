@@ -226,3 +226,17 @@ def test_precomputed_table_device_api(gpu, oracle_cpp):
         got = tab.batch_multi_scalar_multiplication(msms)
         for pairs, g in zip(msms, got):
             assert g == b.native_msm([s for s, _ in pairs], [P[i] for _, i in pairs])
+
+
+def test_fused_wait_timeout_is_redone(gpu, oracle_cpp, monkeypatch):
+    """k_batch_fused's Horner waves wait on window flags of their own launch; a wait that gives up
+    (forced here: SVGPU_BATCH_WAIT_SPINS=0) makes the call redo the batch by the two-kernel path and
+    still return the oracle's results, never SV_ERR_DEVICE (msm_batch.hip)."""
+    import svgpu
+    sizes = [64] * 128
+    B, S, off = _ragged(oracle_cpp, sizes, 4242)
+    exp = _expected(oracle_cpp, B, S, off)
+    monkeypatch.setenv("SVGPU_BATCH_WAIT_SPINS", "0")
+    assert svgpu.msm_batch_arrays(B, S, off) == exp
+    monkeypatch.delenv("SVGPU_BATCH_WAIT_SPINS")
+    assert svgpu.msm_batch_arrays(B, S, off) == exp

@@ -70,3 +70,39 @@ def test_concurrent_decide_key_churn(gpu):
     with ThreadPoolExecutor(max_workers=6) as ex:
         results = list(ex.map(job, range(84)))
     assert all(got == exp for got, exp in results), results
+
+
+def test_concurrent_batches_with_big_msms(gpu, oracle_cpp):
+    """Batched small MSMs (the fused bucket + Horner launch, whose Horner waves wait on flags of
+    their own launch) from several threads at once, beside concurrent 2^20 MSMs on the same GPU:
+    at most one fused launch per device is in flight, the rest take the two-kernel path, and every
+    call returns the oracle's answer."""
+    import svgpu
+    from svgpu.loader import msm_arrays
+    n = 1 << 20
+    BB = oracle_cpp.gen_bases(b.SEED_BASES, n)
+    SB = oracle_cpp.gen_scalars(b.SEED_SCALARS, n)
+    big = b.g1_from_bytes(oracle_cpp.msm_pippenger(BB, SB, 0).tobytes())
+    batches = []
+    for k in range(3):
+        sizes = [64] * 128 if k < 2 else [17, 200, 64, 255] * 40
+        tot = sum(sizes)
+        B = oracle_cpp.gen_bases(b.SEED_BASES, tot, start=50000 * (k + 1))
+        S = oracle_cpp.gen_scalars(b.SEED_SCALARS, tot, start=70000 * (k + 1))
+        off = [0]
+        for m in sizes:
+            off.append(off[-1] + m)
+        exp = [b.g1_from_bytes(oracle_cpp.msm_pippenger(B[lo:hi], S[lo:hi], 1).tobytes())
+               for lo, hi in zip(off[:-1], off[1:])]
+        batches.append((B, S, off, exp))
+
+    def job(i):
+        if i % 4 == 3:
+            return ("msm", msm_arrays(BB, SB) == big)
+        B, S, off, exp = batches[i % 3]
+        return ("batch", svgpu.msm_batch_arrays(B, S, off) == exp)
+
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        results = list(ex.map(job, range(40)))
+    bad = [(i, kind) for i, (kind, ok) in enumerate(results) if not ok]
+    assert not bad, bad

@@ -36,3 +36,16 @@ def test_length_mismatch_panics():
     import svgpu
     with pytest.raises(svgpu.ReferencePanic):
         svgpu.multi_scalar_multiplication([1, 2], [b.G1_GEN])
+
+
+def test_g2_cache_key_accepts_nested_lists():
+    """A G2 point given as nested lists (accepted by enc.g2_struct) keys the per-key struct cache
+    too (an unhashable list key broke decide())."""
+    from svgpu import device as dv
+    from oracle import bn254 as b
+    q = b.G2_GEN
+    as_lists = [[q[0][0], q[0][1]], [q[1][0], q[1][1]]]
+    a = dv._g2_struct_cached(as_lists, 0)
+    c = dv._g2_struct_cached(q, 0)
+    assert bytes(a) == bytes(c)
+    assert dv._g2_struct_cached(as_lists, 0) is a or bytes(dv._g2_struct_cached(as_lists, 0)) == bytes(a)

@@ -472,6 +472,10 @@ def main():
             "window_bits": stats["window_bits"],
             "windows": stats["num_windows"],
             "parallelism": "point-sharded x%d" % world,
+            "dist": ({"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                      "exchange": "all_gather_into_tensor of 96-B Jacobian partials + rank-order fold; "
+                                  "decider: MIN all-reduce of first_fail"}
+                     if world > 1 else {"backend": None, "world_size": 1}),
         },
         "kzg": {
             "pairings_per_s": pairings_per_s,

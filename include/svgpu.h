@@ -250,6 +250,8 @@ typedef struct {
   float total_ms, digits_ms, sort_ms, accumulate_ms, fixup_ms, reduce_ms, host_ms;
   uint32_t window_bits, num_windows, accumulate_launch_units;
   uint64_t entries;
+  float accumulate_span_ms;        /* first accumulate launch's start to the last one's end */
+  uint32_t accumulate_launches;    /* 2 when the window halves run as separate launches */
 } sv_msm_stats;
 int sv_msm_last_stats(sv_msm_stats* out) SV_NOEXCEPT;
 /* Kernel time (HIP events on the call's stream) of the calling thread's last decider launch. */

@@ -318,9 +318,14 @@ inline F2 f2m(const F2& a, const F2& b) {
 }
 inline F2 f2mf(const F2& a, const F& s) { return {qm(a.c0, s), qm(a.c1, s)}; }
 inline F2 f2conj(const F2& a) { return {a.c0, fneg(FQ, a.c1)}; }
-inline F2 f2xi(const F2& a) {
-  F nine = qsmall(9);
-  return {qs(qm(a.c0, nine), a.c1), qa(a.c0, qm(a.c1, nine))};
+inline F nine_times(const F& a) {  // 9a = 8a + a by additions (no product)
+  F t = qa(a, a);
+  t = qa(t, t);
+  t = qa(t, t);
+  return qa(t, a);
+}
+inline F2 f2xi(const F2& a) {  // (9 + u) a by additions, as halo2curves' mul_by_nonresidue
+  return {qs(nine_times(a.c0), a.c1), qa(a.c0, nine_times(a.c1))};
 }
 inline bool f2zero(const F2& a) { return fzero(a.c0) && fzero(a.c1); }
 F2 f2inv(const F2& a) {
@@ -579,6 +584,163 @@ F12 final_exp(const F12& f0) {
   return f12m(f12m(f12m(l0, frob(l1, 1)), frob(l2, 2)), frob(f, 3));
 }
 
+// ---- halo2curves-structured restatement of decide, for the roofline's work count -------------
+// The reference's pairing (halo2curves 0.3.1 bn256, external) works with: Karatsuba Fq2 / Fq6 /
+// Fq12 products (3 / 18 / 54 Fq products), complex Fq2 squaring (2), Fq12 complex squaring (two
+// Fq6 products, 36), the sparse line product mul_by_034 (13 Fq2 products) after scaling the line by
+// the G1 point (4 Fq products), Granger-Scott cyclotomic squaring in the hard part (9 Fq2
+// squarings, 18), exp_by_x (64 cyclotomic squarings + a product per set bit of x) and the Scott et
+// al. hard-part chain; G2Prepared::from runs inside every decide (decider.rs:64).  Restated here
+// with this oracle's own line formulas (dbl/add steps with complex squarings) so that the Fq
+// products of one decide can be COUNTED (or_count_decide_fpmul_h2c) instead of estimated.
+namespace h2c {
+inline F2 f2sq(const F2& a) {
+  const F t = qm(qa(a.c0, a.c1), qs(a.c0, a.c1));
+  const F u = qm(a.c0, a.c1);
+  return {t, qa(u, u)};
+}
+inline F2 f2dbl(const F2& a) { return f2a(a, a); }
+F6 f6_mul_by_01(const F6& a, const F2& c0, const F2& c1) {
+  const F2 aa = f2m(a.c0, c0), bb = f2m(a.c1, c1);
+  const F2 t1 = f2a(f2xi(f2s(f2m(c1, f2a(a.c1, a.c2)), bb)), aa);
+  const F2 t3 = f2a(f2s(f2m(c0, f2a(a.c0, a.c2)), aa), bb);
+  const F2 t2 = f2s(f2s(f2m(f2a(c0, c1), f2a(a.c0, a.c1)), aa), bb);
+  return {t1, t2, t3};
+}
+// f * (c0 + (c3 + c4 v) w)
+F12 mul_by_034(const F12& f, const F2& c0, const F2& c3, const F2& c4) {
+  const F6 t0 = {f2m(f.c0.c0, c0), f2m(f.c0.c1, c0), f2m(f.c0.c2, c0)};
+  const F6 t1 = f6_mul_by_01(f.c1, c3, c4);
+  const F6 t2 = f6_mul_by_01(f6a(f.c0, f.c1), f2a(c0, c3), c4);
+  return {f6a(t0, f6v(t1)), f6s(f6s(t2, t0), t1)};
+}
+F12 sq(const F12& a) {  // complex squaring: two Fq6 products
+  const F6 ab = f6m(a.c0, a.c1);
+  const F6 c0 = f6s(f6s(f6m(f6a(a.c0, a.c1), f6a(a.c0, f6v(a.c1))), ab), f6v(ab));
+  return {c0, f6a(ab, ab)};
+}
+// Granger-Scott: f^2 for f in the cyclotomic subgroup.  w-basis g0..g5 = c0.c0, c1.c0, c0.c1, c1.c1,
+// c0.c2, c1.c2; pairs (g0, g3), (g2, g5), (g1, g4) are Fq4 = Fq2[s]/(s^2 - xi), s = w^3:
+//   A' = 3 A^2 - 2 conj(A), B' = 3 s C^2 + 2 conj(B), C' = 3 B^2 - 2 conj(C)
+F12 cyc_sq(const F12& f) {
+  auto fp4 = [](const F2& x, const F2& y, F2& r0, F2& r1) {  // (x + y s)^2 = r0 + r1 s
+    const F2 t0 = f2sq(x), t1 = f2sq(y);
+    r0 = f2a(f2xi(t1), t0);
+    r1 = f2s(f2s(f2sq(f2a(x, y)), t0), t1);
+  };
+  const F2 g0 = f.c0.c0, g1 = f.c1.c0, g2 = f.c0.c1, g3 = f.c1.c1, g4 = f.c0.c2, g5 = f.c1.c2;
+  F2 a0, a3, b0, b1, c0, c1;
+  fp4(g0, g3, a0, a3);  // A^2
+  fp4(g2, g5, b0, b1);  // C^2 (C = g2 + g5 s)
+  fp4(g1, g4, c0, c1);  // B^2 (B = g1 + g4 s)
+  auto three = [](const F2& x) { return f2a(f2dbl(x), x); };
+  const F2 o0 = f2s(three(a0), f2dbl(g0)), o3 = f2a(three(a3), f2dbl(g3));
+  const F2 o1 = f2a(three(f2xi(b1)), f2dbl(g1)), o4 = f2s(three(b0), f2dbl(g4));
+  const F2 o2 = f2s(three(c0), f2dbl(g2)), o5 = f2a(three(c1), f2dbl(g5));
+  return {{o0, o2, o4}, {o1, o3, o5}};
+}
+F12 exp_by_x(const F12& f) {
+  const uint64_t X = 4965661367192848881ull;
+  F12 r = f12one();
+  for (int i = 63; i >= 0; i--) {
+    r = cyc_sq(r);
+    if ((X >> i) & 1) r = f12m(r, f);
+  }
+  return r;
+}
+F12 final_exp(const F12& f0) {
+  F12 f1 = f12conj(f0), f2 = f12inv(f0);
+  F12 r = f12m(f1, f2);
+  f2 = r;
+  r = f12m(frob(r, 2), f2);
+  const F12 fp = frob(r, 1), fp2 = frob(r, 2), fp3 = frob(fp2, 1);
+  const F12 fu = exp_by_x(r), fu2 = exp_by_x(fu), fu3 = exp_by_x(fu2);
+  F12 y3 = frob(fu, 1);
+  const F12 fu2p = frob(fu2, 1), fu3p = frob(fu3, 1), y2 = frob(fu2, 2);
+  const F12 y0 = f12m(f12m(fp, fp2), fp3);
+  const F12 y1 = f12conj(r), y5 = f12conj(fu2);
+  y3 = f12conj(y3);
+  const F12 y4 = f12conj(f12m(fu, fu2p));
+  F12 y6 = f12conj(f12m(fu3, fu3p));
+  y6 = f12m(f12m(cyc_sq(y6), y4), y5);
+  F12 t1 = f12m(f12m(y3, y5), y6);
+  y6 = f12m(y6, y2);
+  t1 = cyc_sq(f12m(cyc_sq(t1), y6));
+  F12 t0 = f12m(t1, y1);
+  t1 = f12m(t1, y0);
+  return f12m(cyc_sq(t0), t1);
+}
+Line dbl_step(G2P& T) {
+  const Consts& c = *g_c;
+  const F2 a = f2mf(f2m(T.X, T.Y), c.two_inv);
+  const F2 b = f2sq(T.Y), cc = f2sq(T.Z);
+  const F2 e = f2m(c.twist_b, f2a(f2a(cc, cc), cc));
+  const F2 f = f2a(f2a(e, e), e);
+  const F2 g = f2mf(f2a(b, f), c.two_inv);
+  const F2 h = f2s(f2sq(f2a(T.Y, T.Z)), f2a(b, cc));
+  const F2 i = f2s(e, b), j = f2sq(T.X), e2 = f2sq(e);
+  T.X = f2m(a, f2s(b, f));
+  T.Y = f2s(f2sq(g), f2a(f2a(e2, e2), e2));
+  T.Z = f2m(b, h);
+  return {f2n(h), f2a(f2a(j, j), j), i};
+}
+Line add_step(G2P& T, const G2A& Q) {
+  const F2 theta = f2s(T.Y, f2m(Q.y, T.Z)), lambda = f2s(T.X, f2m(Q.x, T.Z));
+  const F2 cc = f2sq(theta), d = f2sq(lambda);
+  const F2 e = f2m(lambda, d), f = f2m(T.Z, cc), g = f2m(T.X, d);
+  const F2 h = f2s(f2a(e, f), f2a(g, g));
+  T.X = f2m(lambda, h);
+  T.Y = f2s(f2m(theta, f2s(g, h)), f2m(e, T.Y));
+  T.Z = f2m(T.Z, e);
+  const F2 j = f2s(f2m(theta, Q.x), f2m(lambda, Q.y));
+  return {lambda, f2n(theta), j};
+}
+std::vector<Line> prepare(const G2A& Q) {
+  const Consts& c = *g_c;
+  std::vector<Line> out;
+  G2P T = {Q.x, Q.y, {fone(FQ), F{{0, 0, 0, 0}}}};
+  const G2A nQ = {Q.x, f2n(Q.y)};
+  for (size_t i = c.naf.size() - 1; i-- > 0;) {
+    out.push_back(h2c::dbl_step(T));
+    if (c.naf[i] == 1) out.push_back(h2c::add_step(T, Q));
+    else if (c.naf[i] == -1) out.push_back(h2c::add_step(T, nQ));
+  }
+  const G2A Q1 = {f2m(f2conj(Q.x), c.frob_x), f2m(f2conj(Q.y), c.frob_y)};
+  const G2A Q2 = {f2m(f2conj(Q1.x), c.frob_x), f2n(f2m(f2conj(Q1.y), c.frob_y))};
+  out.push_back(h2c::add_step(T, Q1));
+  out.push_back(h2c::add_step(T, Q2));
+  return out;
+}
+void ell(F12& f, const Line& l, const A& p) { f = mul_by_034(f, f2mf(l.c0, p.y), f2mf(l.c3, p.x), l.c4); }
+F12 miller(const std::vector<std::pair<A, const std::vector<Line>*>>& terms) {
+  const Consts& c = *g_c;
+  F12 f = f12one();
+  size_t k = 0;
+  const size_t L = c.naf.size();
+  for (size_t i = L - 1; i >= 1; i--) {
+    if (i != L - 1) f = h2c::sq(f);
+    for (auto& t : terms) h2c::ell(f, (*t.second)[k], t.first);
+    k++;
+    if (c.naf[i - 1] != 0) {
+      for (auto& t : terms) h2c::ell(f, (*t.second)[k], t.first);
+      k++;
+    }
+  }
+  for (int s = 0; s < 2; s++) {
+    for (auto& t : terms) h2c::ell(f, (*t.second)[k], t.first);
+    k++;
+  }
+  return f;
+}
+F12 decide_gt(const G2A& g2, const G2A& neg_sg2, const A& lhs, const A& rhs) {
+  const std::vector<Line> l1 = h2c::prepare(g2), l2 = h2c::prepare(neg_sg2);
+  std::vector<std::pair<A, const std::vector<Line>*>> terms;
+  if (!lhs.inf) terms.push_back({lhs, &l1});
+  if (!rhs.inf) terms.push_back({rhs, &l2});
+  return h2c::final_exp(h2c::miller(terms));
+}
+}  // namespace h2c
+
 G2A load_g2(const uint64_t* q) {
   G2A r;
   memcpy(r.x.c0.l, q, 32);
@@ -723,6 +885,30 @@ uint64_t or_count_decide_fpmul(const uint64_t* g2, const uint64_t* s_g2, const u
   g_count_on = true;
   (void)decide_gt(q1, q2, l, r);
   g_count_on = false;
+  return g_fq_muls;
+}
+
+// The same count for the halo2curves-structured restatement (h2c above): the roofline's work unit.
+// gt_out (optional, 12 x 4 u64 canonical) receives its Gt value (the same element as decide_gt's:
+// both final exponentiations are exact).
+uint64_t or_count_decide_fpmul_h2c(const uint64_t* g2, const uint64_t* s_g2, const uint64_t* lhs, const uint64_t* rhs,
+                                   uint64_t* gt_out) {
+  init_consts();
+  G2A q1 = load_g2(g2), q2 = load_g2(s_g2);
+  q2.y = f2n(q2.y);
+  const A l = load_aff(lhs), r = load_aff(rhs);
+  g_fq_muls = 0;
+  g_count_on = true;
+  const F12 e = h2c::decide_gt(q1, q2, l, r);
+  g_count_on = false;
+  if (gt_out) {
+    const F2* c[6] = {&e.c0.c0, &e.c0.c1, &e.c0.c2, &e.c1.c0, &e.c1.c1, &e.c1.c2};
+    for (int k = 0; k < 6; k++) {
+      F a = ffrom(FQ, c[k]->c0), b = ffrom(FQ, c[k]->c1);
+      memcpy(gt_out + k * 8, a.l, 32);
+      memcpy(gt_out + k * 8 + 4, b.l, 32);
+    }
+  }
   return g_fq_muls;
 }
 

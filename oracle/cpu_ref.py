@@ -29,6 +29,8 @@ def lib():
                                     ctypes.POINTER(c_int32), c_void_p]
         L.or_count_decide_fpmul.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p]
         L.or_count_decide_fpmul.restype = c_uint64
+        L.or_count_decide_fpmul_h2c.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+        L.or_count_decide_fpmul_h2c.restype = c_uint64
         L.or_accumulate.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p]
         L.or_gen_scalars.argtypes = [c_uint64, c_uint64, c_size_t, c_void_p]
         L.or_gen_scalars.restype = None
@@ -76,6 +78,16 @@ def count_decide_fpmul(g2: np.ndarray, s_g2: np.ndarray, lhs_row, rhs_row) -> in
     """Fq multiplications of one decide as restated in bn254_ref.cpp (decider roofline)."""
     g2, s_g2, l, r = _c(g2), _c(s_g2), _c(lhs_row), _c(rhs_row)
     return int(lib().or_count_decide_fpmul(g2.ctypes.data, s_g2.ctypes.data, l.ctypes.data, r.ctypes.data))
+
+
+def count_decide_fpmul_h2c(g2: np.ndarray, s_g2: np.ndarray, lhs_row, rhs_row):
+    """(Fq products, Gt value) of one decide in the halo2curves-structured restatement of
+    bn254_ref.cpp (namespace h2c): the decider roofline's work unit, counted."""
+    g2, s_g2, l, r = _c(g2), _c(s_g2), _c(lhs_row), _c(rhs_row)
+    gt = np.zeros(48, dtype=np.uint64)
+    n = int(lib().or_count_decide_fpmul_h2c(g2.ctypes.data, s_g2.ctypes.data, l.ctypes.data, r.ctypes.data,
+                                            gt.ctypes.data))
+    return n, gt
 
 
 def accumulate(lhs, rhs, r: np.ndarray):

@@ -351,10 +351,13 @@ __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scal
                                                      uint32_t nblk, uint32_t* __restrict__ bcnt,
                                                      uint32_t* __restrict__ err, const G1Aff* __restrict__ bases,
                                                      uint4* __restrict__ phix, int phi64, int check_bases,
-                                                     int xcd, int bm) {
+                                                     int xcd, int bm, uint32_t w0, uint32_t nw) {
   using D = Digits<C, GLV>;
   constexpr int W = D::W, LOGB = C - 1;
   constexpr int CB = coarse_bits(C, D::NB), FB = LOGB - CB, NBIN = 1 << CB;
+  // windows [w0, w0 + nw) only (the MSM's window halves are sorted separately, see msm_run_impl):
+  // keys (w - w0) * NBIN + bin
+  const uint32_t nk = nw * NBIN;
   __shared__ uint32_t h[W * NBIN];
   for (int k = threadIdx.x; k < W * NBIN; k += kBlock) h[k] = 0;
   __syncthreads();
@@ -374,14 +377,14 @@ __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scal
     D d;
     d.load(scalars, i, mont_in, err);
     d.each([&](int w, uint32_t mag, uint32_t, uint32_t) {
-      if (mag) atomicAdd(&h[w * NBIN + ((mag - 1) >> FB)], 1u);
+      if (mag && (uint32_t)w - w0 < nw) atomicAdd(&h[(w - w0) * NBIN + ((mag - 1) >> FB)], 1u);
     });
   }
   __syncthreads();
-  // bm: block-major bcnt[blk * NK + (w * NBIN + bin)], one contiguous 4-KB row per block (the scan
-  // reads it in 32-key tiles); else key-major bcnt[(w * NBIN + bin) * nblk + blk] (round 2)
-  for (int k = threadIdx.x; k < W * NBIN; k += kBlock)
-    bcnt[bm ? (size_t)blk * (W * NBIN) + k : (size_t)k * nblk + blk] = h[k];
+  // bm: block-major bcnt[blk * nk + key], one contiguous row per block (the scan reads it in
+  // 32-key tiles); else key-major bcnt[key * nblk + blk] (round 2)
+  for (uint32_t k = threadIdx.x; k < nk; k += kBlock)
+    bcnt[bm ? (size_t)blk * nk + k : (size_t)k * nblk + blk] = h[k];
 }
 
 // one 256-thread block per (window, bin): exclusive scan over blocks in place, total -> btot
@@ -486,10 +489,12 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
                                                         uint32_t nblk, const uint32_t* __restrict__ bcnt,
                                                         const uint32_t* __restrict__ btot,
                                                         const uint32_t* __restrict__ bstart,
-                                                        uint64_t* __restrict__ tmp, int e32, int xcd, int bm) {
+                                                        uint64_t* __restrict__ tmp, int e32, int xcd, int bm,
+                                                        uint32_t w0, uint32_t nw) {
   using D = Digits<C, GLV>;
   constexpr int W = D::W, LOGB = C - 1;
   constexpr int CB = coarse_bits(C, D::NB), FB = LOGB - CB, NBIN = 1 << CB, NK = W * NBIN;
+  const uint32_t nk = nw * NBIN;  // keys of windows [w0, w0 + nw), (w - w0) * NBIN + bin
   // staged entry: local point (LP bits) | half << LP | sign << (LP + 1) | fine << (LP + 2) | (window, bin) key << (LP + 2 + FB)
   constexpr int LP = ceil_log2((int)sort_chunk(D::EP));
   static_assert(LP + 2 + FB + ceil_log2(NK) <= 32, "staged entry overflows 32 bits");
@@ -500,9 +505,13 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
   __shared__ uint32_t part[kBlock];
   __shared__ uint32_t stage[CH * D::EP];  // see the layout above (no separate key array: 3 blocks per CU)
   const uint32_t blk = sort_block(blockIdx.x, gridDim.x, xcd), lo = blk * CH, hi = min(n, lo + CH);
-  for (int k = threadIdx.x; k < NK; k += kBlock) {
-    const size_t at = bm ? (size_t)blk * NK + k : (size_t)k * nblk + blk;
-    off[k] = (blk + 1 < nblk ? bcnt[bm ? at + NK : at + 1] : btot[k]) - bcnt[at];
+  for (uint32_t k = threadIdx.x; k < NK; k += kBlock) {
+    if (k >= nk) {
+      off[k] = 0;
+      continue;
+    }
+    const size_t at = bm ? (size_t)blk * nk + k : (size_t)k * nblk + blk;
+    off[k] = (blk + 1 < nblk ? bcnt[bm ? at + nk : at + 1] : btot[k]) - bcnt[at];
   }
   D dg[PT];
 #pragma unroll
@@ -519,9 +528,9 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
     const uint32_t li = threadIdx.x + j * kBlock;
     if (lo + li < hi) {
       dg[j].each([&](int w, uint32_t mag, uint32_t neg, uint32_t half) {
-        if (mag) {
+        if (mag && (uint32_t)w - w0 < nw) {
           const uint32_t b = mag - 1;
-          const uint32_t k = w * NBIN + (b >> FB);
+          const uint32_t k = (w - w0) * NBIN + (b >> FB);
           const uint32_t pos = atomicAdd(&cur[k], 1u);
           stage[pos] = li | (half << LP) | (neg << (LP + 1)) | ((b & FMASK) << (LP + 2)) | (k << (LP + 2 + FB));
         }
@@ -530,8 +539,8 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
   }
   __syncthreads();
   // global position of local slot x = gbase[key] + x  (cur[] reused for gbase)
-  for (int k = threadIdx.x; k < NK; k += kBlock)
-    cur[k] = bstart[k] + bcnt[bm ? (size_t)blk * NK + k : (size_t)k * nblk + blk] - off[k];
+  for (uint32_t k = threadIdx.x; k < nk; k += kBlock)
+    cur[k] = bstart[k] + bcnt[bm ? (size_t)blk * nk + k : (size_t)k * nblk + blk] - off[k];
   __syncthreads();
   for (uint32_t x = threadIdx.x; x < total; x += kBlock) {
     const uint32_t e = stage[x];
@@ -1440,11 +1449,13 @@ struct SortOut {
 static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, const G1Aff* bases,
                     const Fr* scalars, size_t m, int mont_in, int device, hipStream_t st, uint4* phix,
                     uint32_t nsplit, int check_bases, hipEvent_t ev_sort_mid, hipStream_t side = nullptr,
-                    hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr) {
+                    hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr, uint32_t w0 = 0,
+                    uint32_t nw = 0) {
   const int LOGB = p.c - 1;
   const int nb = p.glv ? 128 : 255;
   const uint32_t CB = (uint32_t)coarse_bits(p.c, nb), FB = (uint32_t)LOGB - CB, NBIN = 1u << CB;
-  const uint32_t nwb = p.W * NBIN;
+  if (nw == 0) nw = p.W;  // windows [w0, w0 + nw); so's buckets are those windows' (w - w0) * B + b
+  const uint32_t nwb = nw * NBIN;
   const uint32_t npts = (uint32_t)m;  // real points (GLV: 2 m virtual ones)
   const uint32_t ep = p.glv ? 2 * p.W : p.W;
   const uint32_t nblk = cdiv(npts, sort_chunk((int)ep));
@@ -1456,7 +1467,7 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
   // block-major per-block counts + the tiled scan (SVGPU_SORT_BM=0: key-major, k_bin_scan_chunks)
   static const int bm = !getenv("SVGPU_SORT_BM") || atoi(getenv("SVGPU_SORT_BM")) != 0 ? 1 : 0;
   SV_LAUNCH_C(k_bin_hist, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.err, bases,
-              phix, p.phi64, check_bases, xcd, bm);
+              phix, p.phi64, check_bases, xcd, bm, w0, nw);
   SV_HIP(hipGetLastError());
   if (ev_sort_mid) SV_HIP(hipEventRecord(ev_sort_mid, st));
   if (bm)
@@ -1465,9 +1476,9 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
     hipLaunchKernelGGL(k_bin_scan_chunks, dim3(nwb), dim3(kBlock), 0, st, w.bcnt, nblk, w.btot);
   // (fusing this scan into k_bin_scan_chunks' last block -- device-scope fence + counter -- was
   // measured 12 -> 122 us for that kernel: the fence writes back the XCD's L2)
-  hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, w.btot, nwb, w.bstart, so.gst + p.nbt);
+  hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, w.btot, nwb, w.bstart, so.gst + (size_t)nw * p.B);
   SV_LAUNCH_C(k_bin_scatter, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.btot, w.bstart,
-              w.tmp, e32, xcd, bm);
+              w.tmp, e32, xcd, bm, w0, nw);
   static thread_local int fine_attr_dev = -1;  // the > 64 KiB dynamic-LDS opt-in, once per thread/device
   if (fine_attr_dev != device) {
     SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort<0>),
@@ -1511,20 +1522,21 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
 // bucket's owner segment from it; otherwise complete buckets are stored and empty ones left alone).
 static int msm_acc(const MsmPlan& p, const MsmScratch& w, const SortOut& so, const G1Aff* bases, int add_into,
                    hipStream_t st, G1Xyzz* bsum, const uint4* phix, uint32_t nsplit, hipEvent_t ev_acc_done,
-                   hipEvent_t ev_fix_mid) {
+                   hipEvent_t ev_fix_mid, uint32_t nbt = 0) {
+  if (nbt == 0) nbt = p.nbt;  // the buckets so covers (a window half: its windows' buckets)
   // (a point prefetch one entry ahead, k_accumulate<., 2>, measured no gain on the device path or
   // on the host-fed pieces' ~2 waves per SIMD: 2^20 host-fed 2.69-2.71 ms either way)
   if (add_into)
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_accumulate<true>), dim3(cdiv(so.T, kBlock)), dim3(kBlock), 0, st, bases,
-                       so.ent, so.gst, so.tstart, p.nbt, so.K, so.T, bsum, w.pfirst, w.plast, w.multi, w.nmulti,
+                       so.ent, so.gst, so.tstart, nbt, so.K, so.T, bsum, w.pfirst, w.plast, w.multi, w.nmulti,
                        w.heavy, w.nheavy, phix, nsplit, p.phi64);
   else
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_accumulate<false>), dim3(cdiv(so.T, kBlock)), dim3(kBlock), 0, st, bases,
-                       so.ent, so.gst, so.tstart, p.nbt, so.K, so.T, bsum, w.pfirst, w.plast, w.multi, w.nmulti,
+                       so.ent, so.gst, so.tstart, nbt, so.K, so.T, bsum, w.pfirst, w.plast, w.multi, w.nmulti,
                        w.heavy, w.nheavy, phix, nsplit, p.phi64);
   SV_HIP(hipGetLastError());
   if (ev_acc_done) SV_HIP(hipEventRecord(ev_acc_done, st));
-  const uint32_t gm = std::min<uint32_t>(cdiv(p.nbt, kBlock), 1024);
+  const uint32_t gm = std::min<uint32_t>(cdiv(nbt, kBlock), 1024);
   hipLaunchKernelGGL(k_fixup, dim3(gm + 256), dim3(kBlock), 0, st, so.gst, so.K, w.pfirst, w.plast, w.multi,
                      w.nmulti, w.heavy, w.nheavy, gm, bsum);
   SV_HIP(hipGetLastError());
@@ -1624,6 +1636,19 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   }
   const uint64_t entries = (uint64_t)n * ep;              // all pieces
   const uint64_t piece_entries = (uint64_t)max_piece * ep;  // the sort scratch, reused per piece
+  // Device-resident inputs: the windows in two halves A = [0, WA), B = [WA, W), each sorted,
+  // accumulated and reduced on its own, so that half B's sort (LDS / memory bound) runs on the sort
+  // stream beside half A's accumulate (VALU bound), and half A's bucket reduction (latency bound)
+  // beside half B's accumulate.  SVGPU_MSM_SPLIT=0 keeps one pass over all windows.
+  static const bool split_env = !getenv("SVGPU_MSM_SPLIT") || atoi(getenv("SVGPU_MSM_SPLIT")) != 0;
+  const bool split = !feed && split_env && p.W >= 2 && p.tree == 1 && n >= (size_t(1) << 16);
+  const uint32_t nwh[2] = {split ? p.W / 2 : p.W, split ? p.W - p.W / 2 : 0};
+  uint32_t Th[2] = {0, 0};
+  if (split) {
+    for (int h = 0; h < 2; h++) Th[h] = cdiv((uint64_t)p.npts * nwh[h], p.K);
+    tst_total = (uint64_t)Th[0] + 1 + Th[1] + 1;
+    Tmax = Th[0] + Th[1];
+  }
 
   // ---- workspace layout
   const int nb = p.glv ? 128 : 255;
@@ -1645,7 +1670,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   add((size_t)nwb * 4);                       // btot
   add(((size_t)nwb + 1) * 4);                 // bstart
   add(piece_entries * 8);                     // tmp (coarse-binned entries)
-  add(((size_t)p.nbt + 1) * 4 * pieces);      // gst per piece
+  add((((size_t)p.nbt + 1) * pieces + 1) * 4);  // gst per piece (+ 1: two window halves)
   add(entries * 4);                           // ent (every piece's sorted entries)
   add(tst_total * 4);                         // tstart per piece
   add((size_t)Tmax * sizeof(G1Xyzz) * 2);     // pfirst, plast
@@ -1681,7 +1706,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   w.btot = ws->carve<uint32_t>(nwb);
   w.bstart = ws->carve<uint32_t>((size_t)nwb + 1);
   w.tmp = ws->carve<uint64_t>(piece_entries);
-  uint32_t* gst_all = ws->carve<uint32_t>(((size_t)p.nbt + 1) * pieces);
+  uint32_t* gst_all = ws->carve<uint32_t>(((size_t)p.nbt + 1) * pieces + 1);
   uint32_t* ent_all = ws->carve<uint32_t>(entries);
   uint32_t* tst_all = ws->carve<uint32_t>(tst_total);
   w.pfirst = ws->carve<G1Xyzz>(Tmax);
@@ -1724,9 +1749,10 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
     ~Drain() {
       if (armed) (void)ws->quiesce();
     }
-  } drain{ws, feed != nullptr};
+  } drain{ws, feed != nullptr || split};
   if (!lean) SV_HIP(hipEventRecord(ev[0], st));
   SV_HIP(hipMemsetAsync(w.err, 0, nerr * 4, st));
+  const uint32_t* half_gst[2] = {nullptr, nullptr};  // split: each window half's bucket starts
   if (!feed) {
     if (conv) {
       hipLaunchKernelGGL(k_to_mont_bases, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, st, bases, bases_m, (uint32_t)n,
@@ -1739,10 +1765,46 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
       side = ws->copy_stream;
     }
     const uint32_t nsplit = p.glv ? (uint32_t)n : ~0u;
-    SV_TRY(msm_sort(p, w, so[0], bases, scalars, n, mont_in, device, st, phix, nsplit, mont_in,
-                    detail ? ev[1] : nullptr, side, ev[60], ev[61]));
-    SV_HIP(hipEventRecord(ev[2], st));
-    SV_TRY(msm_acc(p, w, so[0], bases, 0, st, bsum, phix, nsplit, ev[3], detail ? ev[4] : nullptr));
+    if (split) {
+      SV_TRY(ws->ensure_sort_stream());
+      hipStream_t ss = ws->sort_stream;
+      SortOut sh[2];
+      MsmScratch wh[2] = {w, w};
+      for (int h = 0; h < 2; h++) {
+        sh[h].K = p.K;
+        sh[h].T = Th[h];
+        sh[h].ent = ent_all + (h ? (size_t)p.npts * nwh[0] : 0);  // at most npts entries per window
+        sh[h].gst = gst_all + (h ? (size_t)nwh[0] * p.B + 1 : 0);
+        sh[h].tstart = tst_all + (h ? Th[0] + 1 : 0);
+        wh[h].pfirst = w.pfirst + (h ? Th[0] : 0);
+        wh[h].plast = w.plast + (h ? Th[0] : 0);
+        wh[h].heavy = w.heavy + (h ? nwh[0] * p.B : 0);
+        wh[h].multi = w.multi + (h ? nwh[0] * p.B : 0);
+        wh[h].nheavy = w.err + 1 + 2 * h;
+        wh[h].nmulti = w.err + 2 + 2 * h;
+      }
+      // half A on the compute stream: sort (with the GLV table and the base check), accumulate
+      SV_TRY(msm_sort(p, w, sh[0], bases, scalars, n, mont_in, device, st, phix, nsplit, mont_in,
+                      detail ? ev[1] : nullptr, nullptr, nullptr, nullptr, 0, nwh[0]));
+      SV_HIP(hipEventRecord(ev[2], st));
+      SV_HIP(hipStreamWaitEvent(ss, ev[2], 0));  // the sort scratch is free, the GLV table written
+      SV_TRY(msm_acc(p, wh[0], sh[0], bases, 0, st, bsum, phix, nsplit, ev[3], detail ? ev[4] : nullptr,
+                     nwh[0] * p.B));
+      // half B on the sort stream, beside A's accumulate
+      SV_TRY(msm_sort(p, w, sh[1], bases, scalars, n, mont_in, device, ss, nullptr, nsplit, 0, nullptr, nullptr,
+                      nullptr, nullptr, nwh[0], nwh[1]));
+      SV_HIP(hipEventRecord(ev[62], ss));
+      SV_TRY(msm_acc(p, wh[1], sh[1], bases, 0, ss, bsum + (size_t)nwh[0] * p.B, phix, nsplit, ev[63], nullptr,
+                     nwh[1] * p.B));
+      SV_HIP(hipEventRecord(ev[8], ss));
+      half_gst[0] = sh[0].gst;
+      half_gst[1] = sh[1].gst;
+    } else {
+      SV_TRY(msm_sort(p, w, so[0], bases, scalars, n, mont_in, device, st, phix, nsplit, mont_in,
+                      detail ? ev[1] : nullptr, side, ev[60], ev[61]));
+      SV_HIP(hipEventRecord(ev[2], st));
+      SV_TRY(msm_acc(p, w, so[0], bases, 0, st, bsum, phix, nsplit, ev[3], detail ? ev[4] : nullptr));
+    }
   } else {
     // Piece k: the copy stream stages its scalars, then its bases (the pageable copy blocks this
     // thread, so the piece's sort is queued in between and runs during the base transfer); the sort
@@ -1861,15 +1923,24 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)(2 * kTreeRow)));
       tree_attr_dev = device;
     }
-    const uint32_t* gs = pieces > 1 ? nullptr : so[0].gst;
-    if (p.tree == 2)
-      hipLaunchKernelGGL(k_wsum_tree<false>, dim3(p.J / kTreeN * p.W), dim3(kTreeN), kTreeRow, st, bsum, gs, p.B,
-                         p.J, 1u, tree_out);
-    else
-      hipLaunchKernelGGL(k_wsum_tree<true>, dim3(p.J / kTreeN * p.W), dim3(kTreeN), 2 * kTreeRow, st, bsum, gs, p.B,
-                         p.J, 1u << p.logL, tree_out);
-    hipLaunchKernelGGL(k_group_fin, dim3(p.W * p.NG), dim3(128), 0, st, tree_out, p.J / kTreeN, p.NG,
-                       p.tree == 2 ? 1u : 0u, ping);
+    // windows [w0, w0 + nw) of the bucket sums xb (starts gs: empty buckets skipped) -> ping rows
+    auto reduce_windows = [&](const G1Xyzz* xb, const uint32_t* gs, uint32_t w0, uint32_t nw) {
+      if (p.tree == 2)
+        hipLaunchKernelGGL(k_wsum_tree<false>, dim3(p.J / kTreeN * nw), dim3(kTreeN), kTreeRow, st, xb, gs, p.B,
+                           p.J, 1u, tree_out);
+      else
+        hipLaunchKernelGGL(k_wsum_tree<true>, dim3(p.J / kTreeN * nw), dim3(kTreeN), 2 * kTreeRow, st, xb, gs,
+                           p.B, p.J, 1u << p.logL, tree_out);
+      hipLaunchKernelGGL(k_group_fin, dim3(nw * p.NG), dim3(128), 0, st, tree_out, p.J / kTreeN, p.NG,
+                         p.tree == 2 ? 1u : 0u, ping + (size_t)w0 * p.NG);
+    };
+    if (split) {
+      reduce_windows(bsum, half_gst[0], 0, nwh[0]);  // beside half B's accumulate
+      SV_HIP(hipStreamWaitEvent(st, ev[8], 0));
+      reduce_windows(bsum + (size_t)nwh[0] * p.B, half_gst[1], nwh[0], nwh[1]);
+    } else {
+      reduce_windows(bsum, pieces > 1 ? nullptr : so[0].gst, 0, p.W);
+    }
   } else {
     hipLaunchKernelGGL(k_wsum, dim3(cdiv((uint64_t)p.J * p.W, kBlock)), dim3(kBlock), 0, st, bsum,
                        pieces > 1 ? nullptr : so[0].gst, p.B, p.J, 1u << p.logL, p.W, 1, racc, rtot);
@@ -1917,9 +1988,21 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
     (void)hipEventElapsedTime(&ms, ev[3], ev[5]);
     s.reduce_ms = ms;
   }
-  // host-fed: "accumulate" spans the first piece's accumulate to the last piece's (transfers included)
+  // host-fed: "accumulate" spans the first piece's accumulate to the last piece's (transfers included);
+  // split: the two halves' accumulate launches, each from its own start to its own end (they may
+  // overlap in time), and accumulate_span_ms from the first start to the last end
   (void)hipEventElapsedTime(&ms, ev[2], ev[3]);
   s.accumulate_ms = ms;
+  s.accumulate_span_ms = ms;
+  s.accumulate_launches = 1;
+  if (split) {
+    float mb = 0, mspan = 0;
+    (void)hipEventElapsedTime(&mb, ev[62], ev[63]);
+    (void)hipEventElapsedTime(&mspan, ev[2], ev[63]);
+    s.accumulate_ms = ms + mb;
+    s.accumulate_span_ms = std::max(ms, mspan);
+    s.accumulate_launches = 2;
+  }
   s.host_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
   if (lean) {
     s.total_ms = -1.0f;

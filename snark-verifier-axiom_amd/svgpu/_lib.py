@@ -78,7 +78,7 @@ class sv_msm_stats(Structure):
         ("total_ms", c_float), ("digits_ms", c_float), ("sort_ms", c_float), ("accumulate_ms", c_float),
         ("fixup_ms", c_float), ("reduce_ms", c_float), ("host_ms", c_float),
         ("window_bits", c_uint32), ("num_windows", c_uint32), ("accumulate_launch_units", c_uint32),
-        ("entries", c_uint64),
+        ("entries", c_uint64), ("accumulate_span_ms", c_float), ("accumulate_launches", c_uint32),
     ]
 
 

@@ -84,6 +84,8 @@ pub struct SvMsmStats {
     pub num_windows: u32,
     pub accumulate_launch_units: u32,
     pub entries: u64,
+    pub accumulate_span_ms: f32,
+    pub accumulate_launches: u32,
 }
 
 #[link(name = "svgpu")]

@@ -81,3 +81,26 @@ def test_decide_fpmul_count_is_the_bench_constant():
                                      L[0], R[0])
     src = open(os.path.join(ROOT, "bench.py")).read()
     assert int(re.search(r"FPMUL_RESTATEMENT = (\d+)", src).group(1)) == cnt
+
+
+def test_decide_fpmul_h2c_count_is_the_bench_denominator_and_gt_agrees(oracle_cpp):
+    """bench.py's FPMUL_H2C_COUNTED (the decider roofline's work unit) is the Fq-product count of the
+    halo2curves-structured restatement (bn254_ref.cpp namespace h2c: cyclotomic squarings, sparse
+    034 lines, exp_by_x, Scott et al. hard part), and that restatement's Gt value equals the plain
+    restatement's for accepted and rejected accumulators alike (decider.rs:60-68)."""
+    import re
+    from oracle import cpu_ref
+    from svgpu import encoding as enc
+    g2, sg2, accs = b.gen_decider_case(3, bad=[1])
+    G2, SG2 = np.frombuffer(b.g2_bytes(g2), np.uint64), np.frombuffer(b.g2_bytes(sg2), np.uint64)
+    L = enc.bases_array([a[0] for a in accs])
+    R = enc.bases_array([a[1] for a in accs])
+    ff, gts = oracle_cpp.decide_all(G2, SG2, L, R, threads=1, want_gt=True)
+    assert ff == 1
+    counts = set()
+    for i in range(3):
+        cnt, gt = cpu_ref.count_decide_fpmul_h2c(G2, SG2, L[i], R[i])
+        counts.add(cnt)
+        assert (gt == gts[i]).all()
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert counts == {int(re.search(r"FPMUL_H2C_COUNTED = (\d+)", src).group(1))}

@@ -722,8 +722,13 @@ __device__ __forceinline__ bool join_in_block(uint32_t gs, uint32_t ge, uint32_t
   const uint32_t t0 = gs / K, t1 = (ge - 1) / K;
   return t1 == t0 + 1 && t0 / kBlock == t1 / kBlock;
 }
+// SV_ACC_MIN_BLOCKS: resident 256-thread blocks per CU the register allocator must allow (default 1:
+// no constraint; the kernel takes 146 VGPRs = 3 waves per SIMD)
+#ifndef SV_ACC_MIN_BLOCKS
+#define SV_ACC_MIN_BLOCKS 1
+#endif
 template <bool ADD, int PF = SV_ACC_PREFETCH>
-__global__ void __launch_bounds__(kBlock) k_accumulate(
+__global__ void __launch_bounds__(kBlock, SV_ACC_MIN_BLOCKS) k_accumulate(
     const G1Aff* __restrict__ bases, const uint32_t* __restrict__ ent, const uint32_t* __restrict__ gst,
     const uint32_t* __restrict__ tstart, uint32_t nbt, uint32_t K, uint32_t T,
     G1Xyzz* __restrict__ bsum, G1Xyzz* __restrict__ pfirst, G1Xyzz* __restrict__ plast,
@@ -1636,11 +1641,15 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   }
   const uint64_t entries = (uint64_t)n * ep;              // all pieces
   const uint64_t piece_entries = (uint64_t)max_piece * ep;  // the sort scratch, reused per piece
-  // Device-resident inputs: the windows in two halves A = [0, WA), B = [WA, W), each sorted,
-  // accumulated and reduced on its own, so that half B's sort (LDS / memory bound) runs on the sort
-  // stream beside half A's accumulate (VALU bound), and half A's bucket reduction (latency bound)
-  // beside half B's accumulate.  SVGPU_MSM_SPLIT=0 keeps one pass over all windows.
-  static const bool split_env = !getenv("SVGPU_MSM_SPLIT") || atoi(getenv("SVGPU_MSM_SPLIT")) != 0;
+  // SVGPU_MSM_SPLIT=1 (device-resident inputs; off by default): the windows in two halves
+  // A = [0, WA), B = [WA, W), each sorted, accumulated and reduced on its own, so that half B's sort
+  // runs on the sort stream beside half A's accumulate and half A's reduction beside half B's
+  // accumulate.  Measured slower at 2^20 (round 4, two A/B pairs: 1.89-1.92 vs 1.81-1.82 ms/step):
+  // a half sort costs 0.155 ms, not half of 0.195 (every point's GLV split and digits are still
+  // computed), and the two accumulate launches barely overlap (span 1.47 ms, their own durations
+  // 1.52 ms): k_accumulate holds two 256-thread blocks per CU, so half A's 512 blocks already fill
+  // the chip and half B's wait for them -- one round of blocks each, as the whole launch's two.
+  static const bool split_env = getenv("SVGPU_MSM_SPLIT") && atoi(getenv("SVGPU_MSM_SPLIT")) != 0;
   const bool split = !feed && split_env && p.W >= 2 && p.tree == 1 && n >= (size_t(1) << 16);
   const uint32_t nwh[2] = {split ? p.W / 2 : p.W, split ? p.W - p.W / 2 : 0};
   uint32_t Th[2] = {0, 0};

@@ -276,7 +276,13 @@ WsLease::WsLease(int device, hipStream_t user_stream) {
       ws_ = nullptr;
       return;
     }
-    for (auto& ev : ws_->ev) hipEventCreate(&ev);
+    for (auto& ev : ws_->ev)
+      if (hipEventCreate(&ev) != hipSuccess) {
+        set_error("hipEventCreate failed on device %d", device);
+        delete ws_;  // (its streams and events leak: a device that cannot create events is unusable)
+        ws_ = nullptr;
+        return;
+      }
   }
   ws_->stream = user_stream ? user_stream : ws_->own_stream;
 }

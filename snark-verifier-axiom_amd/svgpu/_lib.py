@@ -129,11 +129,27 @@ PROTOTYPES = [
 ]
 
 
+def _check_fresh():
+    """The library must have been linked from the sources beside it (build/SOURCES.sha256, written
+    by the Makefile): a prebuilt .so that travelled with a changed tree raises here.
+    SVGPU_ALLOW_STALE=1 skips the check (e.g. an A/B library in another directory)."""
+    if os.environ.get("SVGPU_ALLOW_STALE") == "1" or "SVGPU_LIB" in os.environ:
+        return
+    from ._srchash import source_hash
+    stamp = os.path.join(os.path.dirname(LIB_PATH), "SOURCES.sha256")
+    want = source_hash()
+    have = open(stamp).read().strip() if os.path.exists(stamp) else "(no stamp)"
+    if have != want:
+        raise ImportError(f"{LIB_PATH} was not built from the current sources (stamp {have[:16]}, sources "
+                          f"{want[:16]}): rebuild with `make -C snark-verifier-axiom_amd`")
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"libsvgpu.so not found at {LIB_PATH}: build it with `make -C snark-verifier-axiom_amd` "
             "(there is no CPU fallback)")
+    _check_fresh()
     lib = ctypes.CDLL(LIB_PATH)
     for name, res, args in PROTOTYPES:
         fn = getattr(lib, name)

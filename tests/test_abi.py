@@ -170,3 +170,14 @@ def test_accumulate_rejects_unreduced_r_without_compute():
                                               ctypes.byref(out_l), ctypes.byref(out_r))
         assert rc == _lib.SV_ERR_ARG, bad
         assert "not reduced" in _lib.last_error()
+
+
+def test_library_stamp_matches_sources():
+    """build/libsvgpu.so was linked from the sources in this tree (build/SOURCES.sha256, written by
+    the Makefile; svgpu/_lib.py refuses a stale library at import, so a prebuilt .so that travels to
+    the GPU box with changed sources fails loudly instead of testing old code)."""
+    import os
+    from svgpu import _lib, _srchash
+    stamp = os.path.join(os.path.dirname(_lib.LIB_PATH), "SOURCES.sha256")
+    assert open(stamp).read().strip() == _srchash.source_hash()
+    assert any(p.endswith("msm.hip") for p in _srchash.source_files())

@@ -91,6 +91,54 @@ inline E mul(const E& a, const E& b) {
   return reduce_once(t, t[4]);
 }
 
+// Lazily reduced product for the permutation: a, b < 2r gives a result below 2r (4 r^2 < 2^256 r),
+// no final subtraction.  "No-carry" CIOS: r's top word is below 2^63 - 1, so each row's carries fit
+// the N + 1 words (no t[N + 1] word, no extra carry handling).
+inline E mul_lazy(const E& a, const E& b) {
+  uint64_t t[4] = {0, 0, 0, 0};
+  for (int i = 0; i < 4; i++) {
+    u128 s = (u128)a.l[0] * b.l[i] + t[0];
+    uint64_t A = (uint64_t)(s >> 64);
+    t[0] = (uint64_t)s;
+    const uint64_t m = t[0] * NINV;
+    s = (u128)m * MOD[0] + t[0];
+    uint64_t C = (uint64_t)(s >> 64);
+    for (int j = 1; j < 4; j++) {
+      s = (u128)a.l[j] * b.l[i] + t[j] + A;
+      A = (uint64_t)(s >> 64);
+      t[j] = (uint64_t)s;
+      s = (u128)m * MOD[j] + t[j] + C;
+      C = (uint64_t)(s >> 64);
+      t[j - 1] = (uint64_t)s;
+    }
+    t[3] = C + A;
+  }
+  return E{{t[0], t[1], t[2], t[3]}};
+}
+
+// a + b for a, b < 2r, wrapped below 2r (subtract 2r when the sum reaches it)
+inline E add_lazy(const E& a, const E& b) {
+  static constexpr uint64_t M2[4] = {0x87c3eb27e0000002ull, 0x5067d090f372e122ull, 0x70a08b6d0302b0baull,
+                                     0x60c89ce5c2634053ull};  // 2r
+  uint64_t t[4], d[4];
+  u128 c = 0;
+  for (int i = 0; i < 4; i++) {
+    const u128 x = (u128)a.l[i] + b.l[i] + c;
+    t[i] = (uint64_t)x;
+    c = x >> 64;
+  }
+  u128 br = 0;
+  for (int i = 0; i < 4; i++) {
+    const u128 x = (u128)t[i] - M2[i] - br;
+    d[i] = (uint64_t)x;
+    br = (x >> 127) & 1;
+  }
+  const bool ge = c || !br;  // (a + b < 4r < 2^256: c is always 0)
+  E r;
+  for (int i = 0; i < 4; i++) r.l[i] = ge ? d[i] : t[i];
+  return r;
+}
+
 inline E to_mont(const E& a) { return mul(a, E{{R2[0], R2[1], R2[2], R2[3]}}); }
 inline E from_mont(const E& a) { return mul(a, E{{1, 0, 0, 0}}); }
 
@@ -106,9 +154,9 @@ inline bool is_reduced(const E& a) {
   return false;
 }
 
-inline E pow5(const E& x) {
-  const E x2 = mul(x, x);
-  return mul(mul(x2, x2), x);
+inline E pow5(const E& x) {  // x < 2r -> result < 2r
+  const E x2 = mul_lazy(x, x);
+  return mul_lazy(mul_lazy(x2, x2), x);
 }
 
 // the t = 3 constants of poseidon_consts.hpp (8 x u32 Montgomery limbs each) as 4 x u64
@@ -140,31 +188,34 @@ struct Spec3 {
 
 inline void apply_mds3(E (&s)[3], const E* m) {
   E o[3];
-  for (int i = 0; i < 3; i++) o[i] = add(add(mul(s[0], m[3 * i]), mul(s[1], m[3 * i + 1])), mul(s[2], m[3 * i + 2]));
+  for (int i = 0; i < 3; i++)
+    o[i] = add_lazy(add_lazy(mul_lazy(s[0], m[3 * i]), mul_lazy(s[1], m[3 * i + 1])), mul_lazy(s[2], m[3 * i + 2]));
   for (int i = 0; i < 3; i++) s[i] = o[i];
 }
 
 // Poseidon::permutation (poseidon.rs:469-500) after the inputs were added: the bare HADES map in
-// the optimised schedule, as the device's sv::permute<3> runs it (Montgomery form)
+// the optimised schedule, as the device's sv::permute<3> runs it (Montgomery form).  Every word
+// stays below 2r inside (lazy products and sums); the state is canonical again at the end.
 inline void permute3(E (&s)[3]) {
   const Spec3& sp = Spec3::get();
   constexpr int H = Spec3::RF / 2;
-  for (int i = 0; i < 3; i++) s[i] = add(s[i], sp.start[i]);  // absorb_with_pre_constants
+  for (int i = 0; i < 3; i++) s[i] = add_lazy(s[i], sp.start[i]);  // absorb_with_pre_constants
   for (int r = 1; r <= H; r++) {
-    for (int i = 0; i < 3; i++) s[i] = add(pow5(s[i]), sp.start[r * 3 + i]);
+    for (int i = 0; i < 3; i++) s[i] = add_lazy(pow5(s[i]), sp.start[r * 3 + i]);
     apply_mds3(s, r < H ? sp.mds.data() : sp.pre.data());
   }
   for (int r = 0; r < Spec3::RP; r++) {
-    s[0] = add(pow5(s[0]), sp.partial[r]);
+    s[0] = add_lazy(pow5(s[0]), sp.partial[r]);
     const E* row = sp.sparse.data() + r * 5;  // row (3) || col_hat (2)
-    const E s0 = add(add(mul(s[0], row[0]), mul(s[1], row[1])), mul(s[2], row[2]));
-    for (int i = 1; i < 3; i++) s[i] = add(s[i], mul(s[0], row[3 + i - 1]));
+    const E s0 = add_lazy(add_lazy(mul_lazy(s[0], row[0]), mul_lazy(s[1], row[1])), mul_lazy(s[2], row[2]));
+    for (int i = 1; i < 3; i++) s[i] = add_lazy(s[i], mul_lazy(s[0], row[3 + i - 1]));
     s[0] = s0;
   }
   for (int r = 0; r < H; r++) {
-    for (int i = 0; i < 3; i++) s[i] = r < H - 1 ? add(pow5(s[i]), sp.end[r * 3 + i]) : pow5(s[i]);
+    for (int i = 0; i < 3; i++) s[i] = r < H - 1 ? add_lazy(pow5(s[i]), sp.end[r * 3 + i]) : pow5(s[i]);
     apply_mds3(s, sp.mds.data());
   }
+  for (int i = 0; i < 3; i++) s[i] = reduce_once(s[i].l, 0);  // [0, 2r) -> canonical
 }
 
 // Poseidon<Fr, Fr, 3, 2> with the NativeLoader (poseidon.rs:412-467): update buffers, squeeze

@@ -63,7 +63,11 @@ class HostPool {
       std::lock_guard<std::mutex> lk(mu_);
       claim_.store((g << (2 * kIdxBits)) | ((uint64_t)parts << kIdxBits), std::memory_order_release);
     }
-    cv_.notify_all();
+    // wake only the workers the job can use (a 2-slice job -- the accumulation's two MSMs -- used
+    // to wake all 15, each then spinning ~1 ms for a next job: CPU the calling thread's serial work,
+    // e.g. create_proof's host sponge, competes with under the box's CPU quota); workers still
+    // spinning from a burst see the new word without a wake-up
+    for (size_t k = 1; k < parts; k++) cv_.notify_one();
     work();
     while (done_.load(std::memory_order_acquire) < parts) std::this_thread::yield();
   }

@@ -197,3 +197,22 @@ def test_create_proof_rejects_identity_and_empty(gpu):
         svgpu.KzgAs.create_proof(inst)
     with pytest.raises(ReferencePanic):
         svgpu.KzgAs.create_proof([])
+
+
+def test_gt_equals_halo2curves_structured_restatement(gpu, oracle_cpp):
+    """The kernel's Gt value equals the one of the C++ restatement that follows halo2curves'
+    structure (bn254_ref.cpp namespace h2c: complex / Granger-Scott cyclotomic squarings, sparse
+    034 lines, exp_by_x and the Scott et al. hard-part chain) -- accepted and rejected accumulators
+    alike (decider.rs:60-68; the reference's final_exponentiation, external)."""
+    from oracle import cpu_ref
+    from svgpu import device as dv, encoding as enc
+    g2, sg2, accs = b.gen_decider_case(4, seed=0x6767, bad=[1, 3])
+    ff, _, gts = dv.decide(g2, sg2, _dev([a[0] for a in accs], gpu), _dev([a[1] for a in accs], gpu), want_gt=True)
+    assert ff == 1
+    G2, SG2 = np.frombuffer(b.g2_bytes(g2), np.uint64), np.frombuffer(b.g2_bytes(sg2), np.uint64)
+    L = enc.bases_array([a[0] for a in accs])
+    R = enc.bases_array([a[1] for a in accs])
+    for i in range(4):
+        _, gt = cpu_ref.count_decide_fpmul_h2c(G2, SG2, L[i], R[i])
+        limbs = [sum(int(gt[8 * c + 4 * h + j]) << (64 * j) for j in range(4)) for c in range(6) for h in range(2)]
+        assert gts[i] == limbs, i

@@ -939,7 +939,29 @@ struct WOp {
   uint8_t code, imm;
   uint16_t dst, a, b;
 };
-constexpr uint16_t kOpD = 1u << 14, kOpM = 2u << 14;
+constexpr uint16_t kOpD = 1u << 14, kOpM = 2u << 14, kOpY = 3u << 14;  // (tag 3: a paired-step product Y)
+
+// Round 4: TWO Miller steps per multiplication.  f <- (f^2 X_j)^2 X_{j+1} = f^4 Y_p with
+// Y_p = X_j^2 X_{j+1}, X the steps' multipliers (pair products D / merged products M).  The Y_p do
+// not depend on f, so the prologue forms all 32 of them in parallel (pair_steps: one output
+// coefficient per lane, two rounds of Fq2 products); the loop then runs 2 squares + 1 product per
+// pair instead of 2 + 2, 32 fewer Fq12 operations on the chain.
+struct StepTab {
+  uint16_t x[ATE_NAF_LEN];  // step multipliers in loop order; x[0] is the first step's (a copy)
+  int n;
+  int m_final;  // merged product of the two Frobenius steps
+};
+constexpr StepTab make_steps() {
+  StepTab t{};
+  int m = 0, idx = 0;
+  for (int i = ATE_NAF_LEN - 1; i >= 1; i--) {
+    t.x[t.n++] = ATE_NAF[i - 1] != 0 ? (uint16_t)(kOpM | m++) : (uint16_t)(kOpD | idx);
+    idx += ATE_NAF[i - 1] != 0 ? 2 : 1;
+  }
+  t.m_final = m;
+  return t;
+}
+constexpr int kStepPairs = (make_steps().n - 1) / 2;
 enum WSlot {
   S_F0, S_F1, S_FI, S_AC, S_NN, S_NI, S_TAB, S_X0 = S_TAB + 8, S_X1, S_FX, S_FX2, S_FX3, S_A, S_B, S_C, S_B6, S_B12,
   S_B18, S_A6, S_A12, S_A18, S_A30, S_Y, S_Y36, S_L0, S_L1, S_L2, S_T0, S_T1, S_T2, S_E0, S_E1, S_E2, S_GT, kSlots
@@ -979,23 +1001,24 @@ struct WProg {
     }
   }
 };
-constexpr WProg make_wprog() {
+constexpr WProg make_wprog(bool paired = false) {
   WProg P{};
-  const MergeTab mt = make_merges();
-  (void)mt;
-  // Miller loop, merged step multipliers as in k_decide_lanes: f <- f^2 * (D_idx or M_m)
-  int m = 0, idx = 0;
-  for (int i = ATE_NAF_LEN - 1; i >= 1; i--) {
-    const int mul = ATE_NAF[i - 1] != 0 ? (kOpM | m++) : (kOpD | idx);
-    idx += ATE_NAF[i - 1] != 0 ? 2 : 1;
-    if (i == ATE_NAF_LEN - 1) {
-      P.op(OP_COPY, S_F0, mul);
-    } else {
-      P.op(OP_SQR, S_F1, S_F0);
-      P.op(OP_MUL, S_F0, S_F1, mul);
+  const StepTab st = make_steps();
+  P.op(OP_COPY, S_F0, st.x[0]);
+  int j = 1;
+  if (paired) {  // f <- f^4 Y_p (see StepTab)
+    for (int p = 0; p < kStepPairs; p++, j += 2) {
+      P.op(OP_SQR, S_T1, S_F0);
+      P.op(OP_SQR, S_F1, S_T1);
+      P.op(OP_MUL, S_F0, S_F1, kOpY | p);
     }
   }
-  P.op(OP_MUL, S_F1, S_F0, kOpM | m);  // the two Frobenius steps
+  // Miller loop, merged step multipliers as in k_decide_lanes: f <- f^2 * (D_idx or M_m)
+  for (; j < st.n; j++) {
+    P.op(OP_SQR, S_F1, S_F0);
+    P.op(OP_MUL, S_F0, S_F1, st.x[j]);
+  }
+  P.op(OP_MUL, S_F1, S_F0, kOpM | st.m_final);  // the two Frobenius steps
   // Final exponentiation with NO inversion.  The easy part f^(p^6 - 1) = conj(f) / f is kept as the
   // fraction conj(w) / w with w = f: every value of the chain below is a power v^k of
   // v = f^((p^6 - 1)(p^2 + 1)), and v^k = conj(w_k) / w_k where w_k is what the same chain computes
@@ -1052,21 +1075,61 @@ constexpr WProg make_wprog() {
   return P;
 }
 __constant__ WProg c_wprog = make_wprog();
+__constant__ WProg c_wprog2 = make_wprog(true);
+__constant__ StepTab c_steps = make_steps();
 constexpr int kResultSlot = S_E2, kGtSlot = S_GT;
 static_assert(make_wprog().n <= kMaxOps, "decider program too long");
+static_assert(make_wprog(true).n + 32 == make_wprog().n, "pairing saves one product per step pair");
+static_assert(kStepPairs * 6 * sizeof(Fq2) <= (size_t)kSlots * 6 * sizeof(Fq2), "Q fits the slots");
+
+// Y_p = X_j^2 X_{j+1} for every step pair (j = 1 + 2p): Q_p = X_j^2 into Q (the slot region, free
+// during the prologue), then Y_p = Q_p X_{j+1}; one (pair, output coefficient) per lane, Fq2
+// convolutions with the w^6 = xi wrap
+__device__ __forceinline__ const Fq2* step_x(uint16_t o, const Fq2* D, const Fq2* M) {
+  const uint32_t i = o & (kOpD - 1);
+  return (o >> 14) == 2 ? M + 6 * i : D + 6 * i;
+}
+// coefficient k of a * b (w^6 = xi); divergence-free: lanes of one wave hold different k, so every
+// lane forms the same six products (an operand index and a wrap select per term)
+__device__ __forceinline__ Fq2 conv6(const Fq2* a, const Fq2* b, int k) {
+  Fq2 acc = Fq2::zero();
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    const int j = k - i;
+    const bool wrap = j < 0;
+    const Fq2 t = a[i] * b[wrap ? j + 6 : j];
+    const Fq2 tx = fq2_mul_xi(t);
+    acc = acc + (wrap ? tx : t);
+  }
+  return acc;
+}
+__device__ __forceinline__ void pair_steps(Fq2* __restrict__ Q, Fq2* __restrict__ Y, const Fq2* D, const Fq2* M,
+                                           int lane, int lanes) {
+  for (int job = lane; job < kStepPairs * 6; job += lanes) {
+    const int p = job / 6, k = job % 6;
+    const Fq2* x = step_x(c_steps.x[1 + 2 * p], D, M);
+    Q[6 * p + k] = conv6(x, x, k);
+  }
+  __syncthreads();
+  for (int job = lane; job < kStepPairs * 6; job += lanes) {
+    const int p = job / 6, k = job % 6;
+    Y[6 * p + k] = conv6(Q + 6 * p, step_x(c_steps.x[2 + 2 * p], D, M), k);
+  }
+}
 
 constexpr size_t kLdsE = 2 * (size_t)ATE_NUM_LINES * sizeof(LineCoeff);
 constexpr size_t kLdsD = (size_t)ATE_NUM_LINES * 6 * sizeof(Fq2);
 constexpr size_t kLdsSlots = (size_t)kSlots * 6 * sizeof(Fq2);
 constexpr size_t kLdsGamma = sizeof(c_gamma);
 constexpr size_t kLds = kLdsE + kLdsD + kLdsSlots + kLdsGamma;
+static_assert((size_t)(kMaxMerge + kStepPairs) * 6 * sizeof(Fq2) <= kLdsE, "M and Y fit the line region");
 }  // namespace wg
 
 __global__ void __launch_bounds__(wg::kThreads) k_decide_wg(const G1Aff* __restrict__ lhs, const G1Aff* __restrict__ rhs,
                                                           uint32_t n, const LineCoeff* __restrict__ L1,
                                                           const LineCoeff* __restrict__ L2, int mont_in,
                                                           int32_t* __restrict__ verdict, Fq12* __restrict__ gt,
-                                                          const Fq2* __restrict__ kc) {
+                                                          const Fq2* __restrict__ kc, int paired) {
   using namespace wg;
   extern __shared__ __attribute__((aligned(16))) unsigned char dec_lds[];
   __shared__ Fq2 tj[3], di;
@@ -1094,20 +1157,26 @@ __global__ void __launch_bounds__(wg::kThreads) k_decide_wg(const G1Aff* __restr
   __syncthreads();
   merge_products(M, D, t, kThreads);  // (a divergence-free 5-term walk measured no faster)
   __syncthreads();
+  Fq2* Y = M + 6 * kMaxMerge;  // the paired steps' products, behind M in the dead line region
+  if (paired) {
+    pair_steps(S, Y, D, M, t, kThreads);
+    __syncthreads();
+  }
+  const WProg& prog = paired ? c_wprog2 : c_wprog;
   auto opnd = [&](uint16_t o) -> Fq2* {
-    const uint32_t i = o & (kOpD - 1);
-    return (o & kOpM) ? M + 6 * i : ((o & kOpD) ? D + 6 * i : S + 6 * i);
+    const uint32_t i = o & (kOpD - 1), tag = o >> 14;
+    return tag == 3 ? Y + 6 * i : (tag == 2 ? M + 6 * i : (tag == 1 ? D + 6 * i : S + 6 * i));
   };
   const WLane Ln = wlane_init();
 #ifdef SV_WG_PROLOGUE_ONLY
   const int nops = 0;  // timing of the prologue alone (tools/decider_bench.py with SVGPU_LIB)
 #else
-  const int nops = gt ? c_wprog.n : c_wprog.nv;
+  const int nops = gt ? prog.n : prog.nv;
 #endif
-  WOp nxt = c_wprog.ops[0];
+  WOp nxt = prog.ops[0];
   for (int pc = 0; pc < nops; pc++) {
     const WOp op = nxt;
-    if (pc + 1 < nops) nxt = c_wprog.ops[pc + 1];  // next op's scalar load in flight during this one
+    if (pc + 1 < nops) nxt = prog.ops[pc + 1];  // next op's scalar load in flight during this one
     Fq2* dst = S + 6 * op.dst;
     const Fq2* a = opnd(op.a);
     switch (op.code) {
@@ -1272,6 +1341,8 @@ int decide_run_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const vo
   // k_decide_wg's pair products from the key's constants (SVGPU_DECIDER_KC=0: evaluate the lines)
   static const bool kc_env = !getenv("SVGPU_DECIDER_KC") || atoi(getenv("SVGPU_DECIDER_KC")) != 0;
   static const int phases = getenv("SVGPU_DECIDER_PHASES") ? atoi(getenv("SVGPU_DECIDER_PHASES")) : 3;
+  // k_decide_wg's two Miller steps per product (SVGPU_DECIDER_PAIR=0: one per step), read per call
+  const bool pair_env = !getenv("SVGPU_DECIDER_PAIR") || atoi(getenv("SVGPU_DECIDER_PAIR")) != 0;
   const G1Aff* dl = reinterpret_cast<const G1Aff*>(d_lhs);
   const G1Aff* dr = reinterpret_cast<const G1Aff*>(d_rhs);
   const int mont = form == SV_MONTGOMERY ? 1 : 0;
@@ -1284,7 +1355,7 @@ int decide_run_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const vo
   }
   if (lanes == 256)
     hipLaunchKernelGGL(k_decide_wg, dim3((unsigned)n), dim3(wg::kThreads), wg::kLds, st, dl, dr, (uint32_t)n, lines,
-                       L2, mont, d_verdict, d_gt, kc_env ? line_ref->d_kc : nullptr);
+                       L2, mont, d_verdict, d_gt, kc_env ? line_ref->d_kc : nullptr, pair_env ? 1 : 0);
   else if (lanes == 48)
     hipLaunchKernelGGL(k_decide_lanes<8>, dim3((unsigned)n), dim3(64), 0, st, dl, dr, (uint32_t)n, lines, L2, mont,
                        d_verdict, d_gt, phases);

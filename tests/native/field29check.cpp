@@ -1,0 +1,132 @@
+// Test harness (not part of libsvgpu): every operation of csrc/field29.hpp on the host, over random
+// and boundary operands at the bounds the header states; prints "op inputs... output" lines (hex
+// integers) for tests/test_field29.py, which checks values mod p and output bounds with Python ints.
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <initializer_list>
+#include <string>
+
+#include "curve29.hpp"
+
+using namespace sv::r29;
+
+static uint64_t s = 0x9E3779B97F4A7C15ull;
+static int g_top = 23;
+static int n_top_bits() { return g_top; }
+static uint64_t rnd() {
+  s ^= s << 13;
+  s ^= s >> 7;
+  s ^= s << 17;
+  return s;
+}
+// a value below k p: random limbs, then csub down (k p below 2^261), or a boundary value
+static F below(int k, int mode) {
+  F r;
+  if (mode == 1) return zero();
+  if (mode == 2) {  // k p - 1
+    F kp1 = k == 1 ? kp_f<1>() : k == 2 ? kp_f<2>() : k == 4 ? kp_f<4>() : kp_f<6>();
+    F one = zero();
+    one.v[0] = 1;
+    F t = sub<1>(kp1, one);  // kp - 1 + p
+    return csub<1>(t) /* value kp - 1 when k >= 1 */;
+  }
+  for (int i = 0; i < L; i++) r.v[i] = (uint32_t)rnd() & MASK;
+  r.v[L - 1] &= (n_top_bits() == 23 ? 0x7fffffu : 0x3fffffu);  // below 2^255 (~4.4 p) or 2^254
+  return r;
+}
+static void pr(const F& a) {
+  printf(" ");
+  for (int i = L - 1; i >= 0; i--) printf("%08x", a.v[i]);
+}
+// hex integer (below 2^261) -> normalized limbs
+static F parse(const std::string& h) {
+  F r = zero();
+  int bit = 0;
+  for (int k = (int)h.size() - 1; k >= 0 && h[k] != 'x'; k--, bit += 4) {
+    const char c = h[k];
+    const uint32_t d = c <= '9' ? c - '0' : (c | 0x20) - 'a' + 10;
+    r.v[bit / 29] |= (d << (bit % 29)) & MASK;
+    if (bit % 29 > 25) r.v[bit / 29 + 1] |= d >> (29 - bit % 29);
+  }
+  return r;
+}
+// "madd" mode: stdin lines "X Y ZZ ZZZ x2 y2" (hex) -> "X3 Y3 ZZ3 ZZZ3"; "mdbl" lines "x y"
+static int curve_mode(bool dbl) {
+  char buf[6][80];
+  while (true) {
+    const int n = dbl ? scanf("%79s %79s", buf[0], buf[1])
+                      : scanf("%79s %79s %79s %79s %79s %79s", buf[0], buf[1], buf[2], buf[3], buf[4], buf[5]);
+    if (n != (dbl ? 2 : 6)) break;
+    Xyzz r;
+    if (dbl) {
+      r = mdbl(parse(buf[0]), parse(buf[1]));
+    } else {
+      const Xyzz st{parse(buf[0]), parse(buf[1]), parse(buf[2]), parse(buf[3])};
+      r = madd(st, parse(buf[4]), parse(buf[5]));
+    }
+    pr(r.X), pr(r.Y), pr(r.ZZ), pr(r.ZZZ);
+    printf("\n");
+  }
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && !strcmp(argv[1], "madd")) return curve_mode(false);
+  if (argc > 1 && !strcmp(argv[1], "mdbl")) return curve_mode(true);
+  for (int n = 0; n < 3000; n++) {
+    const int mode = n < 40 ? n % 3 : 0;
+    g_top = (n & 1) ? 23 : 22;
+    // raw random below 2^255 (~4.4 p); the Python side knows each op's input bound and checks it
+    F a = below(12, mode), b = below(12, (mode + 1) % 3), c = below(12, mode), d = below(12, (mode + 2) % 3);
+    printf("mul");
+    pr(a), pr(b), pr(mul(a, b));
+    printf("\nsqr");
+    pr(a), pr(sqr(a));
+    printf("\nmul_sum2");
+    pr(a), pr(b), pr(c), pr(d), pr(mul_sum2(a, b, c, d));
+    printf("\nadd");
+    pr(a), pr(b), pr(add(a, b));
+    printf("\nsub2");
+    pr(a), pr(b), pr(sub<2>(a, b));
+    printf("\nsub4");
+    pr(a), pr(b), pr(sub<4>(a, b));
+    printf("\nsub6");
+    pr(a), pr(b), pr(sub<6>(a, b));
+    printf("\ncsub1");
+    pr(a), pr(csub<1>(a));
+    printf("\ncsub2");
+    pr(a), pr(csub<2>(a));
+    printf("\ncsub4");
+    pr(a), pr(csub<4>(a));
+    printf("\nzero6 ");
+    pr(a);
+    printf(" %d", is_zero_mod_p_6p(a) ? 1 : 0);
+    uint32_t w[8], w2[8];
+    to_words(a, w);
+    F back = from_words(w);
+    printf("\nwords");
+    pr(a), pr(back);
+    // conversions (inputs below p as 8 x 32 words: a mod p computed via csub chain)
+    F ar = csub<1>(csub<2>(csub<4>(a)));
+    to_words(ar, w);
+    F r29 = to_r29(w);
+    to_r32(r29, w2);
+    printf("\nto_r29");
+    pr(ar), pr(r29), pr(from_words(w2));
+    F a4 = csub<4>(a);  // below 4p when a is below 8p
+    to_r32(a4, w2);
+    printf("\nto_r32");
+    pr(a4), pr(from_words(w2));
+    printf("\n");
+  }
+  // zero tests on exact multiples of p
+  for (int k = 0; k < 6; k++) {
+    F m = zero();
+    for (int j = 0; j < k; j++) m = sub<1>(m, zero());  // m + p
+    printf("zero6 ");
+    pr(m);
+    printf(" %d\n", is_zero_mod_p_6p(m) ? 1 : 0);
+  }
+  return 0;
+}

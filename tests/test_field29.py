@@ -1,0 +1,146 @@
+"""The 29-bit-limb field and XYZZ mixed addition (csrc/field29.hpp, csrc/curve29.hpp), run on the
+host through tests/native/field29check.cpp and checked with Python integers: every operation's
+value mod p and its stated output bound, and madd / mdbl against the oracle's affine group law
+(oracle/bn254.py), including the identity, doubling and P + (-P) branches.  CPU only."""
+import os
+import random
+import subprocess
+
+import pytest
+
+from oracle import bn254 as ob
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NATIVE = os.path.join(ROOT, "tests", "native")
+BIN = os.path.join(NATIVE, "build", "field29check")
+P = ob.P
+RP = (1 << 261) % P  # R' = 2^261
+RINV = pow(RP, -1, P)
+
+
+@pytest.fixture(scope="module")
+def f29():
+    r = subprocess.run(["make", "-s", "-C", NATIVE, "build/field29check"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return BIN
+
+
+def _limbs(h):
+    """The harness prints a value as its 9 limbs, most significant first, 8 hex digits each."""
+    if len(h) != 72:
+        return int(h, 16)
+    return sum(int(h[8 * i:8 * i + 8], 16) << (29 * (8 - i)) for i in range(9))
+
+
+def test_field_ops_values_and_bounds(f29):
+    out = subprocess.run([f29], capture_output=True, text=True, check=True).stdout
+    counts = {}
+    for line in out.splitlines():
+        f = line.split()
+        op, v = f[0], [_limbs(x) for x in f[1:]]
+        counts[op] = counts.get(op, 0) + 1
+        if op in ("mul", "sqr", "mul_sum2"):
+            bound_in = 12 * P if op != "mul_sum2" else 9 * P
+            ins, r = v[:-1], v[-1]
+            if any(x >= bound_in for x in ins):
+                continue  # outside the stated contract: not checked
+            if op == "mul":
+                want = ins[0] * ins[1]
+            elif op == "sqr":
+                want = ins[0] * ins[0]
+            else:
+                want = ins[0] * ins[1] + ins[2] * ins[3]
+            assert r < 2 * P, line
+            assert r % P == want * RINV % P, line
+        elif op.startswith("sub"):
+            k = int(op[3:])
+            a, b, r = v
+            if b >= k * P:
+                continue
+            assert r == a - b + k * P, line
+        elif op == "add":
+            a, b, r = v
+            assert r == a + b, line
+        elif op.startswith("csub"):
+            k = int(op[4:])
+            a, r = v
+            if a >= 2 * k * P:
+                continue
+            assert r % P == a % P and r < k * P, line
+        elif op == "zero6":
+            a, z = v
+            if a >= 6 * P:
+                continue
+            assert z == (1 if a % P == 0 else 0), line
+        elif op == "words":
+            a, back = v
+            if a < (1 << 256):
+                assert back == a, line
+        elif op == "to_r29":
+            a, r29, back = v
+            assert r29 < 2 * P and r29 % P == a * 32 % P and back == a, line
+        elif op == "to_r32":
+            a, r = v
+            assert r < P and r == a * pow(32, -1, P) % P, line
+    assert counts.get("mul", 0) >= 3000 and counts.get("zero6", 0) >= 3006 and counts.get("to_r32", 0) >= 3000
+
+
+def _state(pt, rng, identity=False):
+    """A random XYZZ representation of an affine point inside the stated bounds (R' form)."""
+    if identity:
+        return (0, 0, 0, 0)
+    x, y = pt
+    z = rng.randrange(1, P)
+    zz, zzz = z * z % P, z * z * z % P
+    X, Y = x * zz % P, y * zzz % P
+    m = lambda v: v * RP % P  # noqa: E731
+    return (m(X) + rng.randrange(4) * P, m(Y) + rng.randrange(2) * P, m(zz) + rng.randrange(2) * P,
+            m(zzz) + rng.randrange(2) * P)
+
+
+def _to_affine(X, Y, ZZ, ZZZ):
+    X, Y, ZZ, ZZZ = (v * RINV % P for v in (X, Y, ZZ, ZZZ))
+    if ZZ == 0:
+        return None
+    return (X * pow(ZZ, -1, P) % P, Y * pow(ZZZ, -1, P) % P)
+
+
+def test_madd_group_law(f29):
+    rng = random.Random(29)
+    g = (1, 2)
+    cases = []  # (state, x2, y2, expected affine sum or None)
+    for n in range(300):
+        a = ob.g1_mul(g, rng.randrange(1, ob.R))
+        b = ob.g1_mul(g, rng.randrange(1, ob.R))
+        kind = n % 10
+        if kind == 7:
+            b = a  # doubling branch
+        elif kind == 8:
+            b = ob.g1_neg(a)  # P + (-P)
+        st = _state(a, rng, identity=(kind == 9))
+        want = b if kind == 9 else ob.g1_add(a, b)
+        xb = b[0] * RP % P + rng.randrange(2) * P
+        yb = b[1] * RP % P + rng.randrange(2) * P
+        cases.append((st, xb, yb, want))
+    inp = "\n".join(" ".join(hex(v) for v in (*st, xb, yb)) for st, xb, yb, _ in cases) + "\n"
+    out = subprocess.run([f29, "madd"], input=inp, capture_output=True, text=True, check=True).stdout.splitlines()
+    assert len(out) == len(cases)
+    for (st, xb, yb, want), line in zip(cases, out):
+        X, Y, ZZ, ZZZ = (_limbs(v) for v in line.split())
+        assert X < 4 * P and Y < 2 * P and ZZ < 2 * P and ZZZ < 2 * P, line
+        got = _to_affine(X, Y, ZZ, ZZZ)
+        assert got == (None if want is None else tuple(want)), (st, xb, yb)
+        if got is None:
+            assert X == Y == ZZ == ZZZ == 0, line  # the identity is exactly zero limbs
+
+
+def test_mdbl(f29):
+    rng = random.Random(30)
+    pts = [ob.g1_mul((1, 2), rng.randrange(1, ob.R)) for _ in range(50)]
+    enc = [(x * RP % P + rng.randrange(2) * P, y * RP % P + rng.randrange(2) * P) for x, y in pts]
+    inp = "\n".join(f"{hex(x)} {hex(y)}" for x, y in enc) + "\n"
+    out = subprocess.run([f29, "mdbl"], input=inp, capture_output=True, text=True, check=True).stdout.splitlines()
+    for pt, line in zip(pts, out):
+        X, Y, ZZ, ZZZ = (_limbs(v) for v in line.split())
+        assert X < 4 * P and Y < 2 * P and ZZ < 2 * P and ZZZ < 2 * P
+        assert _to_affine(X, Y, ZZ, ZZZ) == tuple(ob.g1_add(pt, pt))

@@ -113,6 +113,32 @@ SV_HD G1Xyzz xyzz_madd_2p(const G1Xyzz& p, const Fq& x2, const Fq& y2) {
   const Fq y[2] = {fe_sub2p(Q, X3), fe_neg2p(PPP)};
   return {X3, fe_mul_sum(x, y), fe_mul_lazy(p.ZZ, PP), fe_mul_lazy(p.ZZZ, PPP)};
 }
+// xyzz_madd_2p with the doubling case (p = (x2, y2)) run through the addition's own products, as
+// r29::madd (curve29.hpp): mdbl's U = 2 y2, M = 3 x2^2 become Pd and Rd, (X, Y, ZZ, ZZZ) =
+// (x2, y2, 1, 1), and X3 drops its PPP term -- the rare branch only sets operands.
+SV_HD G1Xyzz xyzz_madd_2p_u(const G1Xyzz& p, const Fq& x2, const Fq& y2) {
+  if (p.is_identity()) return {x2, y2, Fq::one(), Fq::one()};
+  Fq Pd = fe_sub2p(fe_mul_lazy(x2, p.ZZ), p.X);
+  Fq Rd = fe_sub2p(fe_mul_lazy(y2, p.ZZZ), p.Y);
+  Fq X = p.X, Y = p.Y, ZZ = p.ZZ, ZZZ = p.ZZZ;
+  bool dbl = false;
+  if (fe_is_zero2p(Pd)) {
+    if (!fe_is_zero2p(Rd)) return G1Xyzz::identity();
+    const Fq x2s = fe_sqr_hp<FqTag, false>(x2);
+    Pd = fe_add2p(y2, y2);
+    Rd = fe_add2p(fe_add2p(x2s, x2s), x2s);
+    X = x2, Y = y2, ZZ = Fq::one(), ZZZ = Fq::one();
+    dbl = true;
+  }
+  const Fq PP = fe_sqr_hp<FqTag, false>(Pd);
+  const Fq PPP = fe_mul_lazy(Pd, PP);
+  const Fq Q = fe_mul_lazy(X, PP);
+  const Fq R2 = fe_sqr_hp<FqTag, false>(Rd);
+  const Fq X3 = fe_sub2p(fe_sub2p(dbl ? R2 : fe_sub2p(R2, PPP), Q), Q);
+  const Fq x[2] = {Rd, Y};
+  const Fq y[2] = {fe_sub2p(Q, X3), fe_neg2p(PPP)};
+  return {X3, fe_mul_sum(x, y), fe_mul_lazy(ZZ, PP), fe_mul_lazy(ZZZ, PPP)};
+}
 SV_HD G1Xyzz xyzz_canon2p(const G1Xyzz& p) {
   return {fe_canon2p(p.X), fe_canon2p(p.Y), fe_canon2p(p.ZZ), fe_canon2p(p.ZZZ)};
 }

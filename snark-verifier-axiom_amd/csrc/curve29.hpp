@@ -4,7 +4,7 @@
 //   state  X < 4p, Y < 2p, ZZ < 2p, ZZZ < 2p; the identity is exactly all-zero limbs (ZZ == 0: a
 //          non-identity state never has ZZ = 0 mod p, since ZZ3 = ZZ PP and PP != 0 mod p);
 //   point  x2, y2 below 2p (R' form), never the identity (callers skip it).
-// The formulas are add-2008-s / mdbl-2008-s, as xyzz_madd_2p / xyzz_mdbl in curve.hpp.
+// The formulas are madd-2008-s / mdbl-2008-s, as xyzz_madd_2p / xyzz_mdbl in curve.hpp.
 #pragma once
 #include "field29.hpp"
 
@@ -26,32 +26,31 @@ SV29_HD F one() {  // R' mod p
 SV29_HD Xyzz identity() { return {zero(), zero(), zero(), zero()}; }
 SV29_HD bool is_identity(const Xyzz& p) { return is_zero(p.ZZ); }
 
-// 2 (x, y) for an affine point (x, y below 2p)
-SV29_HD Xyzz mdbl(const F& x, const F& y) {
-  const F U = add(y, y);                        // < 4p
-  const F V = sqr(U), W = mul(U, V), S = mul(x, V);  // < 2p
-  const F x2 = sqr(x);
-  const F M = add(add(x2, x2), x2);             // < 6p
-  const F X3 = csub<4>(sub<4>(sqr(M), add(S, S)));  // sqr(M) + 4p - 2S < 6p -> < 4p
-  const F Y3 = mul_sum2(M, sub<4>(S, X3), W, sub<2>(zero(), y));  // M (S - X3) - W y: inputs < 6p
-  return {X3, Y3, V, W};
-}
-
-// p + (x2, y2)
+// p + (x2, y2).  The doubling case (p = (x2, y2)) runs through the same products: mdbl's U = 2 y2,
+// V = U^2, W = U V, S = x2 V, M = 3 x2^2 are the addition's Pd, PP, PPP, Q (with X = x2) and Rd, and
+// X3 = M^2 - 2S, Y3 = M (S - X3) - y2 W, ZZ3 = V, ZZZ3 = W its outputs with (X, Y, ZZ, ZZZ) =
+// (x2, y2, 1, 1) and no PPP term in X3 -- the rare branch only sets operands (one extra square),
+// so the chain holds no registers for a separate doubling (k_accumulate fits 128 VGPRs).
 SV29_HD Xyzz madd(const Xyzz& p, const F& x2, const F& y2) {
   if (is_identity(p)) return {x2, y2, one(), one()};
-  const F U2 = mul(x2, p.ZZ), S2 = mul(y2, p.ZZZ);  // < 2p
-  const F Pd = sub<4>(U2, p.X);  // < 6p
-  const F Rd = sub<2>(S2, p.Y);  // < 4p
+  F Pd = sub<4>(mul(x2, p.ZZ), p.X);   // U2 - X: < 6p
+  F Rd = sub<2>(mul(y2, p.ZZZ), p.Y);  // S2 - Y: < 4p
+  F X = p.X, Y = p.Y, ZZ = p.ZZ, ZZZ = p.ZZZ;
+  bool dbl = false;
   if (is_zero_mod_p_6p(Pd)) {
-    if (is_zero_mod_p_6p(Rd)) return mdbl(x2, y2);
-    return identity();
+    if (!is_zero_mod_p_6p(Rd)) return identity();
+    const F x2s = sqr(x2);
+    Pd = add(y2, y2);               // < 4p
+    Rd = add(add(x2s, x2s), x2s);   // < 6p
+    X = x2, Y = y2, ZZ = one(), ZZZ = one();
+    dbl = true;
   }
-  const F PP = sqr(Pd), PPP = mul(Pd, PP), Q = mul(p.X, PP), R2 = sqr(Rd);  // < 2p
-  const F X3 = csub<4>(sub<4>(sub<2>(R2, PPP), add(Q, Q)));  // (R2 + 2p - PPP) + 4p - 2Q < 8p -> < 4p
-  // Y3 = Rd (Q - X3) - Y PPP, one reduction: inputs Rd < 4p, Q + 4p - X3 < 6p, Y < 2p, 2p - PPP
-  const F Y3 = mul_sum2(Rd, sub<4>(Q, X3), p.Y, sub<2>(zero(), PPP));
-  return {X3, Y3, mul(p.ZZ, PP), mul(p.ZZZ, PPP)};
+  const F PP = sqr(Pd), PPP = mul(Pd, PP), Q = mul(X, PP), R2 = sqr(Rd);  // < 2p
+  // (R2 [+ 2p - PPP]) + 4p - 2Q < 8p -> < 4p
+  const F X3 = csub<4>(sub<4>(dbl ? R2 : sub<2>(R2, PPP), add(Q, Q)));
+  // Y3 = Rd (Q - X3) - Y PPP, one reduction: inputs Rd < 6p, Q + 4p - X3 < 6p, Y < 2p, 2p - PPP
+  const F Y3 = mul_sum2(Rd, sub<4>(Q, X3), Y, sub<2>(zero(), PPP));
+  return {X3, Y3, mul(ZZ, PP), mul(ZZZ, PPP)};
 }
 
 }  // namespace r29

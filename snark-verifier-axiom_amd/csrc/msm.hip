@@ -42,6 +42,7 @@
 #include <vector>
 
 #include "curve.hpp"
+#include "curve29.hpp"
 #include "glv.hpp"
 #include "host_ec.hpp"
 #include "msm.hpp"
@@ -102,6 +103,34 @@ __device__ __forceinline__ void store_xyzz(G1Xyzz* __restrict__ a, uint32_t i, c
   const uint32_t* s = reinterpret_cast<const uint32_t*>(&v);
 #pragma unroll
   for (int k = 0; k < 8; k++) p[k] = make_uint4(s[4 * k], s[4 * k + 1], s[4 * k + 2], s[4 * k + 3]);
+}
+
+// r29w storage form (see AccChain) <-> canonical x R: one coordinate, one point
+__device__ __forceinline__ Fq fq_from_r29w(const Fq& w) {  // x R' words (below 4p) -> x R canonical
+  Fq r;
+  r29::to_r32(r29::from_words(w.v), r.v);
+  return r;
+}
+__device__ __forceinline__ Fq fq_to_r29w(const Fq& c) {  // x R canonical -> x R' words (below 2p)
+  Fq r;
+  r29::to_words(r29::to_r29(c.v), r.v);
+  return r;
+}
+__device__ __forceinline__ G1Xyzz xyzz_from_r29w(const G1Xyzz& a) {
+  return {fq_from_r29w(a.X), fq_from_r29w(a.Y), fq_from_r29w(a.ZZ), fq_from_r29w(a.ZZZ)};
+}
+__device__ __forceinline__ G1Xyzz xyzz_to_r29w(const G1Xyzz& a) {
+  return {fq_to_r29w(a.X), fq_to_r29w(a.Y), fq_to_r29w(a.ZZ), fq_to_r29w(a.ZZZ)};
+}
+__device__ __forceinline__ G1Xyzz load_bucket(const G1Xyzz* __restrict__ a, uint32_t i, int r29w) {
+  G1Xyzz v = load_xyzz(a, i);
+  if (r29w) {
+    v.X = fq_from_r29w(v.X);
+    v.Y = fq_from_r29w(v.Y);
+    v.ZZ = fq_from_r29w(v.ZZ);
+    v.ZZZ = fq_from_r29w(v.ZZZ);
+  }
+  return v;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -722,18 +751,68 @@ __device__ __forceinline__ bool join_in_block(uint32_t gs, uint32_t ge, uint32_t
   const uint32_t t0 = gs / K, t1 = (ge - 1) / K;
   return t1 == t0 + 1 && t0 / kBlock == t1 / kBlock;
 }
-// SV_ACC_MIN_BLOCKS: resident 256-thread blocks per CU the register allocator must allow (default 1:
-// no constraint; the kernel takes 146 VGPRs = 3 waves per SIMD)
+// The accumulator of k_accumulate's chain.  R29 (default): 9 x 29-bit limbs (curve29.hpp; each
+// partial product one v_mad_u64_u32 with no carry add, 125 VGPRs = 4 waves per SIMD), points
+// converted on load (a shift + small reduction, no product).  Its bucket sums are STORED in the
+// chain's own Montgomery form, x R' as 8 words ("r29w": every coordinate is below 4p < 2^256), not
+// converted to field.hpp's canonical x R: a segment end runs for the whole wave whenever one of its
+// lanes ends a segment, so its work counts nearly every iteration (the conversion there cost ~70 us
+// of a 1.39 ms accumulate).  The readers convert instead: k_fixup (loads and stores r29w, so bsum
+// stays uniform for the next host-fed piece) and bucket_at (k_wsum / k_wsum_tree, once per bucket).
+// SVGPU_ACC_R29=0 selects the 8 x 32-bit chain (xyzz_madd_2p_u), stored canonical.
+#ifndef SV_ACC_MADD32
+#define SV_ACC_MADD32 xyzz_madd_2p_u
+#endif
+template <bool R29>
+struct AccChain;
+template <>
+struct AccChain<false> {
+  using T = G1Xyzz;
+  __device__ static T identity() { return G1Xyzz::identity(); }
+  __device__ static T in(const G1Xyzz& a) { return a; }
+  __device__ static G1Xyzz out(const T& a) { return xyzz_canon2p(a); }
+  __device__ static T madd(const T& acc, const G1Aff& p, bool neg) {
+    return SV_ACC_MADD32(acc, p.x, neg ? -p.y : p.y);
+  }
+};
+template <>
+struct AccChain<true> {
+  using T = r29::Xyzz;
+  __device__ static T identity() { return r29::identity(); }
+  __device__ static T in(const G1Xyzz& a) {  // storage form: x R' as words (r29w_*)
+    return {r29::from_words(a.X.v), r29::from_words(a.Y.v), r29::from_words(a.ZZ.v), r29::from_words(a.ZZZ.v)};
+  }
+  __device__ static G1Xyzz out(const T& a) {
+    G1Xyzz r;
+    r29::to_words(a.X, r.X.v);
+    r29::to_words(a.Y, r.Y.v);
+    r29::to_words(a.ZZ, r.ZZ.v);
+    r29::to_words(a.ZZZ, r.ZZZ.v);
+    return r;
+  }
+  __device__ static T madd(const T& acc, const G1Aff& p, bool neg) {
+    const r29::F x = r29::to_r29(p.x.v), y = r29::to_r29(p.y.v);
+    return r29::madd(acc, x, neg ? r29::sub<2>(r29::zero(), y) : y);
+  }
+};
+
+// SV_ACC_MIN_BLOCKS / SV_ACC29_MIN_BLOCKS: resident 256-thread blocks per CU the register allocator
+// must allow for the 8 x 32-bit / 29-bit chains (1: no constraint -- the 32-bit chain takes 144
+// VGPRs = 3 waves per SIMD; 4: at most 128 VGPRs, which the 29-bit chain meets without spilling)
 #ifndef SV_ACC_MIN_BLOCKS
 #define SV_ACC_MIN_BLOCKS 1
 #endif
-template <bool ADD, int PF = SV_ACC_PREFETCH>
-__global__ void __launch_bounds__(kBlock, SV_ACC_MIN_BLOCKS) k_accumulate(
+#ifndef SV_ACC29_MIN_BLOCKS
+#define SV_ACC29_MIN_BLOCKS 4
+#endif
+template <bool ADD, bool R29, int PF = SV_ACC_PREFETCH>
+__global__ void __launch_bounds__(kBlock, R29 ? SV_ACC29_MIN_BLOCKS : SV_ACC_MIN_BLOCKS) k_accumulate(
     const G1Aff* __restrict__ bases, const uint32_t* __restrict__ ent, const uint32_t* __restrict__ gst,
     const uint32_t* __restrict__ tstart, uint32_t nbt, uint32_t K, uint32_t T,
     G1Xyzz* __restrict__ bsum, G1Xyzz* __restrict__ pfirst, G1Xyzz* __restrict__ plast,
     uint32_t* __restrict__ multi, uint32_t* __restrict__ nmulti, uint32_t* __restrict__ heavy,
     uint32_t* __restrict__ nheavy, const uint4* __restrict__ phix, uint32_t nsplit, int phi64) {
+  using A = AccChain<R29>;
   __shared__ G1Xyzz shead[kBlock];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t m = gst[nbt];
@@ -742,7 +821,8 @@ __global__ void __launch_bounds__(kBlock, SV_ACC_MIN_BLOCKS) k_accumulate(
   // owner piece left in acc for the in-block join (g = its bucket), or none
   bool owner = false;
   uint32_t g = 0, gs = 0, ge = 0;
-  G1Xyzz acc = G1Xyzz::identity();
+  G1Xyzz sum;  // the last segment's canonical sum (the owner piece's, for the join)
+  typename A::T acc = A::identity();
   if (active) {
     const uint32_t e_end = min(s0 + K, m);
     g = tstart[t];
@@ -754,7 +834,7 @@ __global__ void __launch_bounds__(kBlock, SV_ACC_MIN_BLOCKS) k_accumulate(
     // starts from the sum the earlier pieces left in bsum (identity-initialised) instead of the
     // identity, so every later join (in block, k_fixup) and store carries it: no extra addition
     if constexpr (ADD) {
-      if (s0 == gs) acc = load_xyzz(bsum, g);
+      if (s0 == gs) acc = A::in(load_xyzz(bsum, g));
     }
     uint32_t vnext = 0;
     if constexpr (PF >= 1) vnext = ent[s0];
@@ -762,12 +842,12 @@ __global__ void __launch_bounds__(kBlock, SV_ACC_MIN_BLOCKS) k_accumulate(
     if constexpr (PF >= 2) pnext = load_vpoint(bases, phix, vnext & 0x7fffffffu, nsplit, phi64);
     for (uint32_t e = s0; e < e_end; e++) {
       if (e >= ge) {  // segment [seg_start, ge) of bucket g ends inside this chunk
-        acc = xyzz_canon2p(acc);
+        const G1Xyzz sum = A::out(acc);
         if (seg_start == gs) {
-          store_xyzz(bsum, g, acc);
+          store_xyzz(bsum, g, sum);
         } else {  // head piece of a bucket owned by an earlier thread
-          if (join_in_block(gs, ge, K)) shead[threadIdx.x] = acc;
-          else store_xyzz(pfirst, t, acc);
+          if (join_in_block(gs, ge, K)) shead[threadIdx.x] = sum;
+          else store_xyzz(pfirst, t, sum);
         }
         first = false;
         do {
@@ -777,8 +857,8 @@ __global__ void __launch_bounds__(kBlock, SV_ACC_MIN_BLOCKS) k_accumulate(
         } while (ge <= e);
         seg_start = e;
         // the new segment starts bucket g (gs == e: entries are contiguous, empty buckets skipped)
-        if constexpr (ADD) acc = load_xyzz(bsum, g);
-        else acc = G1Xyzz::identity();
+        if constexpr (ADD) acc = A::in(load_xyzz(bsum, g));
+        else acc = A::identity();
       }
       uint32_t v;
       G1Aff p;
@@ -797,33 +877,37 @@ __global__ void __launch_bounds__(kBlock, SV_ACC_MIN_BLOCKS) k_accumulate(
           pnext = load_vpoint(bases, phix, vnext & 0x7fffffffu, nsplit, phi64);
         }
       }
-      if (v & 0x80000000u) p.y = -p.y;
-      if (!p.is_identity()) acc = xyzz_madd_2p(acc, p.x, p.y);
+      if (!p.is_identity()) acc = A::madd(acc, p, (v & 0x80000000u) != 0);
     }
-    acc = xyzz_canon2p(acc);
+    sum = A::out(acc);
     if (seg_start == gs && e_end == ge) {
-      store_xyzz(bsum, g, acc);
+      store_xyzz(bsum, g, sum);
     } else if (seg_start != gs) {  // first segment, bucket started earlier (it may also go on later)
-      if (join_in_block(gs, ge, K)) shead[threadIdx.x] = acc;
-      else store_xyzz(pfirst, t, acc);
+      if (join_in_block(gs, ge, K)) shead[threadIdx.x] = sum;
+      else store_xyzz(pfirst, t, sum);
     } else if (join_in_block(gs, ge, K)) {  // this thread owns a two-piece in-block bucket
       owner = true;
     } else {
-      store_xyzz(first ? pfirst : plast, t, acc);
+      store_xyzz(first ? pfirst : plast, t, sum);
       multi[atomicAdd(nmulti, 1u)] = g;  // joined by k_fixup
       if ((ge - 1) / K - gs / K > kFixSerial) heavy[atomicAdd(nheavy, 1u)] = g;
     }
   }
   __syncthreads();
-  if (owner) store_xyzz(bsum, g, xyzz_add(acc, shead[threadIdx.x + 1]));
+  if (owner) {
+    if constexpr (R29)
+      store_xyzz(bsum, g, xyzz_to_r29w(xyzz_add(xyzz_from_r29w(sum), xyzz_from_r29w(shead[threadIdx.x + 1]))));
+    else
+      store_xyzz(bsum, g, xyzz_add(sum, shead[threadIdx.x + 1]));
+  }
 }
 
 // Queued crossing buckets (see k_accumulate): pieces pfirst/plast joined serially when the bucket
 // spans at most kFixSerial + 1 threads; longer ones (skewed digits: all-equal scalars, a short top
 // window) are queued by k_accumulate for k_fixup's heavy blocks instead of being walked serially.
 __device__ __forceinline__ G1Xyzz fixup_head(const G1Xyzz* __restrict__ pfirst, const G1Xyzz* __restrict__ plast,
-                                             uint32_t s, uint32_t t0, uint32_t K) {
-  return (s == t0 * K) ? load_xyzz(pfirst, t0) : load_xyzz(plast, t0);
+                                             uint32_t s, uint32_t t0, uint32_t K, int r29w) {
+  return load_bucket((s == t0 * K) ? pfirst : plast, t0, r29w);
 }
 
 // One launch for both queues: blocks [0, gm) walk the multi queue (grid-stride, one bucket per
@@ -838,7 +922,7 @@ __global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ g
                                                   const uint32_t* __restrict__ nmulti,
                                                   const uint32_t* __restrict__ heavy,
                                                   const uint32_t* __restrict__ nheavy, uint32_t gm,
-                                                  G1Xyzz* __restrict__ bsum) {
+                                                  G1Xyzz* __restrict__ bsum, int r29w) {
   __shared__ G1Xyzz sh[kBlock];
   const uint32_t tid = threadIdx.x;
   if (blockIdx.x < gm) {  // block-uniform
@@ -852,9 +936,16 @@ __global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ g
       const uint32_t s = gst[g], e = gst[g + 1];
       const uint32_t t0 = s / K, t1 = (e - 1) / K;
       if (t1 - t0 > kFixSerial) continue;  // a heavy bucket: the other blocks' part
+      // r29w (k_accumulate's 29-bit chain): pieces and the stored sum in x R' words
       Fq acc = quad::ld(s == t0 * K ? pfirst + t0 : plast + t0, c);
-      for (uint32_t t = t0 + 1; t <= t1; t++) acc = quad::add_2p(acc, quad::ld(pfirst + t, c), c);
-      quad::st(bsum + g, c, fe_canon2p(acc));
+      if (r29w) acc = fq_from_r29w(acc);
+      for (uint32_t t = t0 + 1; t <= t1; t++) {
+        Fq v = quad::ld(pfirst + t, c);
+        if (r29w) v = fq_from_r29w(v);
+        acc = quad::add_2p(acc, v, c);
+      }
+      acc = fe_canon2p(acc);
+      quad::st(bsum + g, c, r29w ? fq_to_r29w(acc) : acc);
     }
     return;
   }
@@ -864,7 +955,7 @@ __global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ g
     const uint32_t s = gst[g], e = gst[g + 1];
     const uint32_t t0 = s / K, t1 = (e - 1) / K;
     G1Xyzz acc = G1Xyzz::identity();
-    for (uint32_t t = t0 + 1 + tid; t <= t1; t += kBlock) acc = xyzz_add(acc, load_xyzz(pfirst, t));
+    for (uint32_t t = t0 + 1 + tid; t <= t1; t += kBlock) acc = xyzz_add(acc, load_bucket(pfirst, t, r29w));
     sh[tid] = acc;
     __syncthreads();
     for (uint32_t st = kBlock / 2; st > 0; st >>= 1) {
@@ -872,7 +963,8 @@ __global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ g
       __syncthreads();
     }
     if (tid == 0) {
-      store_xyzz(bsum, g, xyzz_add(fixup_head(pfirst, plast, s, t0, K), sh[0]));
+      const G1Xyzz sum = xyzz_add(fixup_head(pfirst, plast, s, t0, K, r29w), sh[0]);
+      store_xyzz(bsum, g, r29w ? xyzz_to_r29w(sum) : sum);
     }
     __syncthreads();
   }
@@ -883,9 +975,9 @@ __global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ g
 // instead of in k_fixup was measured 155 -> 440 us for k_wsum at 2^20: ~7 % of buckets cross,
 // so nearly every wave's iteration diverges into the join loop.)
 __device__ __forceinline__ bool bucket_at(const G1Xyzz* __restrict__ x, const uint32_t* __restrict__ gs, uint32_t i,
-                                          G1Xyzz& out) {
+                                          G1Xyzz& out, int r29w) {  // r29w: sums in the 29-bit chain's form
   if (gs && gs[i] == gs[i + 1]) return false;
-  out = load_xyzz(x, i);
+  out = load_bucket(x, i, r29w);
   return true;
 }
 
@@ -894,7 +986,8 @@ __device__ __forceinline__ bool bucket_at(const G1Xyzz* __restrict__ x, const ui
 // Empty buckets (gst[b] == gst[b + 1]) are never written by the accumulate pass and read as identity.
 __global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, const uint32_t* __restrict__ gst,
                                                  uint32_t N, uint32_t J, uint32_t L, uint32_t groups, int base,
-                                                 G1Xyzz* __restrict__ acc_out, G1Xyzz* __restrict__ tot_out) {
+                                                 G1Xyzz* __restrict__ acc_out, G1Xyzz* __restrict__ tot_out,
+                                                 int r29w) {
   uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= J * groups) return;
   uint32_t g = tid / J, j = tid % J;
@@ -908,14 +1001,14 @@ __global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, c
     // reduce 0.404 -> 0.393 ms)
     uint32_t i = hi - 1;
     G1Xyzz nx = G1Xyzz::identity();
-    bool ne = bucket_at(x, gs, i, nx);
+    bool ne = bucket_at(x, gs, i, nx, r29w);
     for (;;) {
       const G1Xyzz cur = nx;
       const bool cne = ne;
       const uint32_t ci = i;
       if (ci > lo) {
         i = ci - 1;
-        ne = bucket_at(x, gs, i, nx);
+        ne = bucket_at(x, gs, i, nx, r29w);
       }
       if (cne) run = xyzz_add_2p(run, cur);
       if (base || ci > lo) acc = xyzz_add_2p(acc, run);
@@ -1140,7 +1233,7 @@ __device__ __forceinline__ uint32_t* tr_task(uint32_t tau, uint32_t np, uint32_t
 template <bool RUN>
 __global__ void __launch_bounds__(kTreeN) k_wsum_tree(const G1Xyzz* __restrict__ X, const uint32_t* __restrict__ gst,
                                                        uint32_t N, uint32_t J, uint32_t L,
-                                                       G1Xyzz* __restrict__ blk_out) {
+                                                       G1Xyzz* __restrict__ blk_out, int r29w) {
   extern __shared__ uint32_t tr_lds[];
   uint32_t* rowT = tr_lds;
   uint32_t* rowA = tr_lds + 32 * kTreeRS;  // RUN only
@@ -1157,14 +1250,14 @@ __global__ void __launch_bounds__(kTreeN) k_wsum_tree(const G1Xyzz* __restrict__
     if (hi > lo) {
       uint32_t i = hi - 1;
       G1Xyzz nx = G1Xyzz::identity();
-      bool ne = bucket_at(x, gs, i, nx);
+      bool ne = bucket_at(x, gs, i, nx, r29w);
       for (;;) {
         const G1Xyzz cur = nx;
         const bool cne = ne;
         const uint32_t ci = i;
         if (ci > lo) {
           i = ci - 1;
-          ne = bucket_at(x, gs, i, nx);
+          ne = bucket_at(x, gs, i, nx, r29w);
         }
         if (cne) run = xyzz_add_2p(run, cur);
         acc = xyzz_add_2p(acc, run);
@@ -1184,7 +1277,7 @@ __global__ void __launch_bounds__(kTreeN) k_wsum_tree(const G1Xyzz* __restrict__
   } else {
     // level 0 over the buckets themselves (odd lanes; an empty bucket is the identity)
     G1Xyzz t = G1Xyzz::identity();
-    if (j < N) bucket_at(x, gs, j, t);
+    if (j < N) bucket_at(x, gs, j, t, r29w);
     const G1Xyzz ot = xor1(t);
     if (odd) {
       tr_put(rowT, tid - 1, xyzz_add_2p(ot, t));
@@ -1522,6 +1615,13 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
   return SV_OK;
 }
 
+// k_accumulate's chain: the 29-bit one (default; bucket sums stored as r29w, see AccChain) or
+// SVGPU_ACC_R29=0 the 32-bit one.  Read once per process: every launch of one MSM agrees.
+static int acc_r29() {
+  static const int r29 = !getenv("SVGPU_ACC_R29") || atoi(getenv("SVGPU_ACC_R29")) != 0;
+  return r29;
+}
+
 // Bucket accumulation of a sorted piece + its crossing-bucket fixups into bsum, on stream st
 // (add_into: the piece's bucket sums are added to what bsum holds -- k_accumulate<true> starts each
 // bucket's owner segment from it; otherwise complete buckets are stored and empty ones left alone).
@@ -1529,21 +1629,19 @@ static int msm_acc(const MsmPlan& p, const MsmScratch& w, const SortOut& so, con
                    hipStream_t st, G1Xyzz* bsum, const uint4* phix, uint32_t nsplit, hipEvent_t ev_acc_done,
                    hipEvent_t ev_fix_mid, uint32_t nbt = 0) {
   if (nbt == 0) nbt = p.nbt;  // the buckets so covers (a window half: its windows' buckets)
-  // (a point prefetch one entry ahead, k_accumulate<., 2>, measured no gain on the device path or
+  // (a point prefetch one entry ahead, k_accumulate<., ., 2>, measured no gain on the device path or
   // on the host-fed pieces' ~2 waves per SIMD: 2^20 host-fed 2.69-2.71 ms either way)
-  if (add_into)
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_accumulate<true>), dim3(cdiv(so.T, kBlock)), dim3(kBlock), 0, st, bases,
-                       so.ent, so.gst, so.tstart, nbt, so.K, so.T, bsum, w.pfirst, w.plast, w.multi, w.nmulti,
-                       w.heavy, w.nheavy, phix, nsplit, p.phi64);
-  else
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_accumulate<false>), dim3(cdiv(so.T, kBlock)), dim3(kBlock), 0, st, bases,
-                       so.ent, so.gst, so.tstart, nbt, so.K, so.T, bsum, w.pfirst, w.plast, w.multi, w.nmulti,
-                       w.heavy, w.nheavy, phix, nsplit, p.phi64);
+  const int r29 = acc_r29();
+  auto kern = add_into ? (r29 ? k_accumulate<true, true> : k_accumulate<true, false>)
+                       : (r29 ? k_accumulate<false, true> : k_accumulate<false, false>);
+  hipLaunchKernelGGL(kern, dim3(cdiv(so.T, kBlock)), dim3(kBlock), 0, st, bases, so.ent, so.gst, so.tstart, nbt,
+                     so.K, so.T, bsum, w.pfirst, w.plast, w.multi, w.nmulti, w.heavy, w.nheavy, phix, nsplit,
+                     p.phi64);
   SV_HIP(hipGetLastError());
   if (ev_acc_done) SV_HIP(hipEventRecord(ev_acc_done, st));
   const uint32_t gm = std::min<uint32_t>(cdiv(nbt, kBlock), 1024);
   hipLaunchKernelGGL(k_fixup, dim3(gm + 256), dim3(kBlock), 0, st, so.gst, so.K, w.pfirst, w.plast, w.multi,
-                     w.nmulti, w.heavy, w.nheavy, gm, bsum);
+                     w.nmulti, w.heavy, w.nheavy, gm, bsum, r29);
   SV_HIP(hipGetLastError());
   if (ev_fix_mid) SV_HIP(hipEventRecord(ev_fix_mid, st));
   return SV_OK;
@@ -1936,10 +2034,10 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
     auto reduce_windows = [&](const G1Xyzz* xb, const uint32_t* gs, uint32_t w0, uint32_t nw) {
       if (p.tree == 2)
         hipLaunchKernelGGL(k_wsum_tree<false>, dim3(p.J / kTreeN * nw), dim3(kTreeN), kTreeRow, st, xb, gs, p.B,
-                           p.J, 1u, tree_out);
+                           p.J, 1u, tree_out, acc_r29());
       else
         hipLaunchKernelGGL(k_wsum_tree<true>, dim3(p.J / kTreeN * nw), dim3(kTreeN), 2 * kTreeRow, st, xb, gs,
-                           p.B, p.J, 1u << p.logL, tree_out);
+                           p.B, p.J, 1u << p.logL, tree_out, acc_r29());
       hipLaunchKernelGGL(k_group_fin, dim3(nw * p.NG), dim3(128), 0, st, tree_out, p.J / kTreeN, p.NG,
                          p.tree == 2 ? 1u : 0u, ping + (size_t)w0 * p.NG);
     };
@@ -1952,7 +2050,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
     }
   } else {
     hipLaunchKernelGGL(k_wsum, dim3(cdiv((uint64_t)p.J * p.W, kBlock)), dim3(kBlock), 0, st, bsum,
-                       pieces > 1 ? nullptr : so[0].gst, p.B, p.J, 1u << p.logL, p.W, 1, racc, rtot);
+                       pieces > 1 ? nullptr : so[0].gst, p.B, p.J, 1u << p.logL, p.W, 1, racc, rtot, acc_r29());
     if (group_quad)
       hipLaunchKernelGGL(k_group_sum_q, dim3(p.NG * p.W * gparts), dim3(kGroupBlock), 0, st, racc, rtot, p.J,
                          p.logJ, gparts, ping, gpart, w.err + 64);

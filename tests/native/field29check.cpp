@@ -51,20 +51,12 @@ static F parse(const std::string& h) {
   }
   return r;
 }
-// "madd" mode: stdin lines "X Y ZZ ZZZ x2 y2" (hex) -> "X3 Y3 ZZ3 ZZZ3"; "mdbl" lines "x y"
-static int curve_mode(bool dbl) {
+// "madd" mode: stdin lines "X Y ZZ ZZZ x2 y2" (hex) -> "X3 Y3 ZZ3 ZZZ3"
+static int madd_mode() {
   char buf[6][80];
-  while (true) {
-    const int n = dbl ? scanf("%79s %79s", buf[0], buf[1])
-                      : scanf("%79s %79s %79s %79s %79s %79s", buf[0], buf[1], buf[2], buf[3], buf[4], buf[5]);
-    if (n != (dbl ? 2 : 6)) break;
-    Xyzz r;
-    if (dbl) {
-      r = mdbl(parse(buf[0]), parse(buf[1]));
-    } else {
-      const Xyzz st{parse(buf[0]), parse(buf[1]), parse(buf[2]), parse(buf[3])};
-      r = madd(st, parse(buf[4]), parse(buf[5]));
-    }
+  while (scanf("%79s %79s %79s %79s %79s %79s", buf[0], buf[1], buf[2], buf[3], buf[4], buf[5]) == 6) {
+    const Xyzz st{parse(buf[0]), parse(buf[1]), parse(buf[2]), parse(buf[3])};
+    const Xyzz r = madd(st, parse(buf[4]), parse(buf[5]));
     pr(r.X), pr(r.Y), pr(r.ZZ), pr(r.ZZZ);
     printf("\n");
   }
@@ -72,8 +64,7 @@ static int curve_mode(bool dbl) {
 }
 
 int main(int argc, char** argv) {
-  if (argc > 1 && !strcmp(argv[1], "madd")) return curve_mode(false);
-  if (argc > 1 && !strcmp(argv[1], "mdbl")) return curve_mode(true);
+  if (argc > 1 && !strcmp(argv[1], "madd")) return madd_mode();
   for (int n = 0; n < 3000; n++) {
     const int mode = n < 40 ? n % 3 : 0;
     g_top = (n & 1) ? 23 : 22;

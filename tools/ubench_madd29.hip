@@ -1,5 +1,5 @@
 // Microbenchmark (round 4): the bucket accumulation's inner step with 9 x 29-bit limbs
-// (csrc/curve29.hpp madd) against the library's xyzz_madd_2p (8 x 32-bit, curve.hpp), in a
+// (csrc/curve29.hpp madd) against the library's xyzz_madd_2p_u (8 x 32-bit, curve.hpp), in a
 // k_accumulate-shaped kernel: each thread walks K consecutive entries of a random index list,
 // loads the 64-byte affine point (x R words, as the library's tables), adds it into a register
 // accumulator, and stores the canonical sum (x R words) at the end.  The r29 kernel converts each
@@ -36,7 +36,7 @@ __global__ void __launch_bounds__(256) k_r32(const uint4* __restrict__ bases, co
     Fq x, y;
     load_pt(bases, v & 0x7fffffffu, x.v, y.v);
     if (v & 0x80000000u) y = -y;
-    acc = xyzz_madd_2p(acc, x, y);
+    acc = xyzz_madd_2p_u(acc, x, y);
   }
   out[t] = xyzz_canon2p(acc);
 }

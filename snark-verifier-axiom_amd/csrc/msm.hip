@@ -106,10 +106,22 @@ __device__ __forceinline__ void store_xyzz(G1Xyzz* __restrict__ a, uint32_t i, c
 }
 
 // r29w storage form (see AccChain) <-> canonical x R: one coordinate, one point
-__device__ __forceinline__ Fq fq_from_r29w(const Fq& w) {  // x R' words (below 4p) -> x R canonical
+// x R' words (below 4p) -> x R canonical: x R = (x R') / 32 mod p, an exact division of w + m p,
+// m = -w p^-1 mod 32 (p = 7 mod 32, -p^-1 = 9): eight v_mad_u64_u32 and eight funnel shifts
+__device__ __forceinline__ Fq fq_from_r29w(const Fq& w) {
+  const uint32_t m = (w.v[0] * 9u) & 31u;
+  uint32_t t[9];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    c = (uint64_t)m * FQ_P[i] + ((uint64_t)w.v[i] + (c >> 32));
+    t[i] = (uint32_t)c;
+  }
+  t[8] = (uint32_t)(c >> 32);
   Fq r;
-  r29::to_r32(r29::from_words(w.v), r.v);
-  return r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = __builtin_amdgcn_alignbit(t[i + 1], t[i], 5);
+  return fe_canon2p(r);  // (w + m p) / 32 < (4p + 31p) / 32 < 2p
 }
 __device__ __forceinline__ Fq fq_to_r29w(const Fq& c) {  // x R canonical -> x R' words (below 2p)
   Fq r;

@@ -1466,6 +1466,9 @@ MsmPlan msm_plan(size_t n) {
   // k_group_sum(_q)
   p.tree = 1;
   if (const char* e = getenv("SVGPU_GROUP_TREE")) p.tree = atoi(e);
+  // k_accumulate's chain (AccChain): the 29-bit one unless SVGPU_ACC_R29=0; fixed per call, so
+  // the accumulate, fixup and reduction launches of one MSM agree on the stored form
+  p.r29 = !getenv("SVGPU_ACC_R29") || atoi(getenv("SVGPU_ACC_R29")) != 0;
   if (p.tree == 2 && p.B % kTreeN == 0 && p.B / kTreeN <= 128) p.logL = 0;
   else if (p.tree == 2) p.tree = 1;
   p.J = p.B >> p.logL;
@@ -1627,13 +1630,6 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
   return SV_OK;
 }
 
-// k_accumulate's chain: the 29-bit one (default; bucket sums stored as r29w, see AccChain) or
-// SVGPU_ACC_R29=0 the 32-bit one.  Read once per process: every launch of one MSM agrees.
-static int acc_r29() {
-  static const int r29 = !getenv("SVGPU_ACC_R29") || atoi(getenv("SVGPU_ACC_R29")) != 0;
-  return r29;
-}
-
 // Bucket accumulation of a sorted piece + its crossing-bucket fixups into bsum, on stream st
 // (add_into: the piece's bucket sums are added to what bsum holds -- k_accumulate<true> starts each
 // bucket's owner segment from it; otherwise complete buckets are stored and empty ones left alone).
@@ -1643,7 +1639,7 @@ static int msm_acc(const MsmPlan& p, const MsmScratch& w, const SortOut& so, con
   if (nbt == 0) nbt = p.nbt;  // the buckets so covers (a window half: its windows' buckets)
   // (a point prefetch one entry ahead, k_accumulate<., ., 2>, measured no gain on the device path or
   // on the host-fed pieces' ~2 waves per SIMD: 2^20 host-fed 2.69-2.71 ms either way)
-  const int r29 = acc_r29();
+  const int r29 = p.r29;
   auto kern = add_into ? (r29 ? k_accumulate<true, true> : k_accumulate<true, false>)
                        : (r29 ? k_accumulate<false, true> : k_accumulate<false, false>);
   hipLaunchKernelGGL(kern, dim3(cdiv(so.T, kBlock)), dim3(kBlock), 0, st, bases, so.ent, so.gst, so.tstart, nbt,
@@ -2046,10 +2042,10 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
     auto reduce_windows = [&](const G1Xyzz* xb, const uint32_t* gs, uint32_t w0, uint32_t nw) {
       if (p.tree == 2)
         hipLaunchKernelGGL(k_wsum_tree<false>, dim3(p.J / kTreeN * nw), dim3(kTreeN), kTreeRow, st, xb, gs, p.B,
-                           p.J, 1u, tree_out, acc_r29());
+                           p.J, 1u, tree_out, p.r29);
       else
         hipLaunchKernelGGL(k_wsum_tree<true>, dim3(p.J / kTreeN * nw), dim3(kTreeN), 2 * kTreeRow, st, xb, gs,
-                           p.B, p.J, 1u << p.logL, tree_out, acc_r29());
+                           p.B, p.J, 1u << p.logL, tree_out, p.r29);
       hipLaunchKernelGGL(k_group_fin, dim3(nw * p.NG), dim3(128), 0, st, tree_out, p.J / kTreeN, p.NG,
                          p.tree == 2 ? 1u : 0u, ping + (size_t)w0 * p.NG);
     };
@@ -2062,7 +2058,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
     }
   } else {
     hipLaunchKernelGGL(k_wsum, dim3(cdiv((uint64_t)p.J * p.W, kBlock)), dim3(kBlock), 0, st, bsum,
-                       pieces > 1 ? nullptr : so[0].gst, p.B, p.J, 1u << p.logL, p.W, 1, racc, rtot, acc_r29());
+                       pieces > 1 ? nullptr : so[0].gst, p.B, p.J, 1u << p.logL, p.W, 1, racc, rtot, p.r29);
     if (group_quad)
       hipLaunchKernelGGL(k_group_sum_q, dim3(p.NG * p.W * gparts), dim3(kGroupBlock), 0, st, racc, rtot, p.J,
                          p.logJ, gparts, ping, gpart, w.err + 64);

@@ -27,6 +27,7 @@ struct MsmPlan {
   size_t npts;      // virtual points: n, or 2n with GLV
   int phi64;        // GLV table: whole phi(P) records (1) or beta x only (0)
   int tree;         // bucket reduction: 0 k_wsum + k_group_sum, 1 running sums + tree, 2 tree over buckets
+  int r29;          // k_accumulate's chain: 29-bit limbs, sums stored as x R' words (1) or 32-bit (0)
 };
 
 MsmPlan msm_plan(size_t n);

@@ -269,3 +269,34 @@ def test_bucket_reduction_paths(gpu, oracle_cpp, monkeypatch, path, glv):
         B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=23)
         S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=23)
         assert svgpu.msm_arrays(B, S) == _to_pt(oracle_cpp.msm_pippenger(B, S, 0)), "2^19"
+
+
+@pytest.mark.parametrize("chain", ["1", "0"])
+def test_accumulate_chains(gpu, oracle_cpp, monkeypatch, chain):
+    """k_accumulate's two chains (SVGPU_ACC_R29: 9 x 29-bit limbs with the sums stored as x R' words
+    and converted by k_fixup / bucket_at, or 8 x 32-bit limbs), with every reader of the stored sums:
+    the default tree, the plain k_wsum reduction, host-fed pieces (ADD mode: owner segments start
+    from the stored sums), repeated points (the doubling folded into the addition), P + (-P), and
+    one skewed bucket (k_fixup's heavy queue), against the reference Pippenger (msm.rs:238-316)."""
+    import svgpu
+    monkeypatch.setenv("SVGPU_ACC_R29", chain)
+    n = 40000
+    B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=77)
+    S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=77)
+    B[100:3000] = B[99]  # one base repeated with equal scalars: same-bucket doublings
+    S[100:3000] = S[99]
+    from svgpu import encoding as enc
+    x, y = enc.g1_from_limbs(B[5000])
+    B[5001] = enc.bases_array([(x, b.P - y)])[0]  # -P with the same scalar: cancels in every bucket
+    S[5001] = S[5000]
+    exp = _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
+    assert svgpu.msm_arrays(B, S, svgpu.SV_CANONICAL) == exp
+    monkeypatch.setenv("SVGPU_GROUP_TREE", "0")
+    assert svgpu.msm_arrays(B, S, svgpu.SV_CANONICAL) == exp
+    monkeypatch.delenv("SVGPU_GROUP_TREE")
+    monkeypatch.setenv("SVGPU_H2D_PIECES", "3")
+    n2 = 1 << 18  # host-fed in pieces (from 2^15 points)
+    B2 = oracle_cpp.gen_bases(b.SEED_BASES, n2, start=3)
+    S2 = oracle_cpp.gen_scalars(b.SEED_SCALARS, n2, start=3)
+    S2[: n2 // 2] = S2[0]  # half the points in one bucket per window
+    assert svgpu.msm_arrays(B2, S2, svgpu.SV_CANONICAL) == _to_pt(oracle_cpp.msm_pippenger(B2, S2, 0))

@@ -293,6 +293,40 @@ __global__ void k_glv_phix(const G1Aff* __restrict__ bases, uint32_t n, uint4* _
   if (i < n) glv_phix(bases, i, phix, phi64, err);
 }
 
+// The 29-bit chain's table of virtual points (p.r29, replaces phix): every record in x R' words
+// (AccChain's storage form), so the accumulate's per-entry point conversion is a limb split --
+// converted once per point here instead of once per bucket entry (16 entries per point at 2^20).
+// P_i at record i and, with GLV, phi(P_i) = (beta x_i, y_i) at record nsplit + i.  With err set the
+// bases are checked to be reduced (Montgomery input is used as is).
+static constexpr int kPhiVtab = 2;  // k_bin_hist's phi64 value for "phix is the r29 table"
+__device__ __forceinline__ void st_words(uint4* o, const Fq& w) {
+  o[0] = make_uint4(w.v[0], w.v[1], w.v[2], w.v[3]);
+  o[1] = make_uint4(w.v[4], w.v[5], w.v[6], w.v[7]);
+}
+__device__ __forceinline__ void vtab_put(const G1Aff* __restrict__ bases, uint32_t i, uint4* __restrict__ vtab,
+                                         uint32_t nsplit, bool glv, uint32_t* __restrict__ err) {
+  const G1Aff a = load_aff(bases, i);
+  if (err && (!a.x.is_reduced() || !a.y.is_reduced())) atomicOr(err, 1u);
+  const Fq y = fq_to_r29w(a.y);
+  uint4* o = vtab + 4 * (size_t)i;
+  st_words(o, fq_to_r29w(a.x));
+  st_words(o + 2, y);
+  if (glv) {
+    Fq beta;
+#pragma unroll
+    for (int j = 0; j < 8; j++) beta.v[j] = GLV_BETA_MONT[j];
+    uint4* q = vtab + 4 * ((size_t)nsplit + i);
+    st_words(q, fq_to_r29w(a.x * beta));
+    st_words(q + 2, y);
+  }
+}
+// Host-fed pieces with the 29-bit chain: the piece's table once its bases have landed
+__global__ void k_vtab(const G1Aff* __restrict__ bases, uint32_t n, uint4* __restrict__ vtab, int glv,
+                       uint32_t* __restrict__ err) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) vtab_put(bases, i, vtab, n, glv != 0, err);
+}
+
 // Montgomery-form bases that no other pass reads before the accumulate (no GLV table, host-fed)
 __global__ void k_check_bases(const G1Aff* __restrict__ bases, uint32_t n, uint32_t* __restrict__ err) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -407,7 +441,9 @@ __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scal
   const uint32_t lo = blk * CH, hi = min(n, lo + CH);
   for (uint32_t i = lo + threadIdx.x; i < hi; i += kBlock) {
     // Montgomery bases are checked here (canonical ones by k_to_mont_bases)
-    if constexpr (GLV) {
+    if (phix && phi64 == kPhiVtab) {  // the 29-bit chain's table (n = nsplit on the device path)
+      vtab_put(bases, i, phix, n, GLV, check_bases ? err : nullptr);
+    } else if constexpr (GLV) {
       if (phix) glv_phix(bases, i, phix, phi64, check_bases ? err : nullptr);  // (null: bases not landed yet, k_glv_phix later)
     } else {
       if (check_bases) {
@@ -803,7 +839,7 @@ struct AccChain<true> {
     return r;
   }
   __device__ static T madd(const T& acc, const G1Aff& p, bool neg) {
-    const r29::F x = r29::to_r29(p.x.v), y = r29::to_r29(p.y.v);
+    const r29::F x = r29::from_words(p.x.v), y = r29::from_words(p.y.v);  // the table's x R' words
     return r29::madd(acc, x, neg ? r29::sub<2>(r29::zero(), y) : y);
   }
 };
@@ -1580,7 +1616,7 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
   // block-major per-block counts + the tiled scan (SVGPU_SORT_BM=0: key-major, k_bin_scan_chunks)
   static const int bm = !getenv("SVGPU_SORT_BM") || atoi(getenv("SVGPU_SORT_BM")) != 0 ? 1 : 0;
   SV_LAUNCH_C(k_bin_hist, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.err, bases,
-              phix, p.phi64, check_bases, xcd, bm, w0, nw);
+              phix, p.r29 ? kPhiVtab : p.phi64, check_bases, xcd, bm, w0, nw);
   SV_HIP(hipGetLastError());
   if (ev_sort_mid) SV_HIP(hipEventRecord(ev_sort_mid, st));
   if (bm)
@@ -1640,6 +1676,11 @@ static int msm_acc(const MsmPlan& p, const MsmScratch& w, const SortOut& so, con
   // (a point prefetch one entry ahead, k_accumulate<., ., 2>, measured no gain on the device path or
   // on the host-fed pieces' ~2 waves per SIMD: 2^20 host-fed 2.69-2.71 ms either way)
   const int r29 = p.r29;
+  if (r29) {  // phix is the 29-bit chain's table of every virtual point (vtab_put): read record idx
+    bases = reinterpret_cast<const G1Aff*>(phix);
+    phix = nullptr;
+    nsplit = ~0u;
+  }
   auto kern = add_into ? (r29 ? k_accumulate<true, true> : k_accumulate<true, false>)
                        : (r29 ? k_accumulate<false, true> : k_accumulate<false, false>);
   hipLaunchKernelGGL(kern, dim3(cdiv(so.T, kBlock)), dim3(kBlock), 0, st, bases, so.ent, so.gst, so.tstart, nbt,
@@ -1774,7 +1815,9 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   auto add = [&](size_t b) { bytes += Workspace::aligned(b); };
   const bool conv = (form == SV_CANONICAL);
   if (conv) add(n * sizeof(G1Aff));
-  if (p.glv) add(n * (p.phi64 ? 4 : 2) * sizeof(uint4));  // GLV: beta x (or phi(P)) per point
+  // GLV: beta x (or phi(P)) per point; the 29-bit chain: its table of every virtual point instead
+  const size_t tab4 = p.r29 ? (p.glv ? 8 : 4) : (p.glv ? (p.phi64 ? 4 : 2) : 0);  // uint4 per point
+  if (tab4) add(n * tab4 * sizeof(uint4));
   const size_t nfinal = (size_t)p.W * p.NG;
   uint32_t gparts = nfinal < 256 ? 2 : 1;      // k_group_sum blocks per group (see there)
   if (const char* e = getenv("SVGPU_GROUP_P")) gparts = (uint32_t)std::max(1, atoi(e));
@@ -1812,7 +1855,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   const Fr* scalars = reinterpret_cast<const Fr*>(d_scalars);
   const int mont_in = form == SV_MONTGOMERY ? 1 : 0;
   G1Aff* bases_m = conv ? ws->carve<G1Aff>(n) : nullptr;
-  uint4* phix = p.glv ? ws->carve<uint4>((p.phi64 ? 4 : 2) * n) : nullptr;
+  uint4* phix = tab4 ? ws->carve<uint4>(tab4 * n) : nullptr;
   MsmScratch w;
   // the group sums and the error flag / counters share one region: one D2H copy reads both
   G1Xyzz* ping = ws->carve<G1Xyzz>(nfinal + (nerr * 4 + sizeof(G1Xyzz) - 1) / sizeof(G1Xyzz));
@@ -1992,7 +2035,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
       Fr* dsc = const_cast<Fr*>(scalars) + lo;
       // GLV: piece-local virtual points (i, m + i) over the piece's bases and its slice of the table
       const uint32_t nsplit = p.glv ? (uint32_t)m : ~0u;
-      uint4* phix_k = p.glv ? phix + (size_t)(p.phi64 ? 4 : 2) * lo : nullptr;
+      uint4* phix_k = tab4 ? phix + tab4 * lo : nullptr;
       SV_TRY(wait_stage(2 * k + 1));
       SV_HIP(hipStreamWaitEvent(ss, sc_ready, 0));
       SV_TRY(msm_sort(p, w, so[k], nullptr, dsc, m, mont_in, device, ss, nullptr, nsplit, 0, nullptr));
@@ -2008,9 +2051,12 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
       if (conv)  // canonical bases converted (and checked) once they have landed
         hipLaunchKernelGGL(k_to_mont_bases, dim3(cdiv(m, kBlock)), dim3(kBlock), 0, ps, db, bases_m + lo,
                            (uint32_t)m, w.err);
+      if (p.r29)  // the piece's table (29-bit chain) from the landed (converted) bases, checked
+        hipLaunchKernelGGL(k_vtab, dim3(cdiv(m, kBlock)), dim3(kBlock), 0, ps, pbases, (uint32_t)m, phix_k,
+                           p.glv ? 1 : 0, conv ? nullptr : w.err);
       else if (!p.glv)
         hipLaunchKernelGGL(k_check_bases, dim3(cdiv(m, kBlock)), dim3(kBlock), 0, ps, db, (uint32_t)m, w.err);
-      if (p.glv)  // the piece's phi table from the landed (converted) bases; Montgomery ones checked
+      if (!p.r29 && p.glv)  // the piece's phi table from the landed (converted) bases; Montgomery ones checked
         hipLaunchKernelGGL(k_glv_phix, dim3(cdiv(m, kBlock)), dim3(kBlock), 0, ps, pbases, (uint32_t)m, phix_k,
                            p.phi64, conv ? nullptr : w.err);
       SV_HIP(hipGetLastError());

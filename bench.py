@@ -469,7 +469,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32 (254-bit Montgomery field, 8x32-bit limbs)",
+        "dtype": "u32 (254-bit Montgomery field: bucket chain 9x29-bit limbs, elsewhere 8x32-bit)",
         "data": "synthetic (SplitMix64 seeded scalars < r, try-and-increment points on y^2=x^3+3)",
         "config": {
             "workload": "BN254 G1 Pippenger MSM, 2^%d random points/scalars per GPU (config 2 at N=1; "

@@ -338,7 +338,7 @@ def main():
             "refs_gather_inclusive_ms": r_s * 1e3,
             "refs_x_device_resident": r_s * 1e3 / dev_ms,
             "h2d_pieces": os.environ.get("SVGPU_H2D_PIECES", os.environ.get(
-                "SVGPU_H2D_SPLIT", "default: 4 equal pieces (msm), 2,2,3,3,3,3 (refs)")),
+                "SVGPU_H2D_SPLIT", "default: 5,4,4,3 (msm), 2,2,3,3,3,3 (refs)")),
             "same_result_as_device_path": bool(h_res == result and r_res == result),
             "note": "sv_bn254_g1_msm: pageable host arrays -> HBM in pieces, staged back to back by the workspace's "
                     "feeder thread; each piece sorted on a second stream once its scalars land and accumulated into "

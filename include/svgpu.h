@@ -69,7 +69,7 @@ const char* sv_version(void) SV_NOEXCEPT;
  * Host buffers.  num_gpus <= 0 means every initialised device (point-sharded, partials
  * folded in device order).  Scalars must be reduced (< r) and base coordinates reduced
  * (< p) in the given form, else SV_ERR_ARG.  The inputs reach HBM in pieces on a copy
- * stream (default: 4 equal pieces from 2^18 points, 2 from 2^15, else 1;
+ * stream (default: 4 pieces weighted 5,4,4,3 from 2^18 points, 2 equal from 2^15, else 1;
  * SVGPU_H2D_PIECES = N equal pieces, SVGPU_H2D_SPLIT = comma-separated weights); each
  * piece is sorted on a second stream once its scalars land and accumulated into the one
  * bucket set once its bases land, while later pieces are in flight; buffers are pooled.   */

@@ -308,15 +308,22 @@ __device__ __forceinline__ void vtab_put(const G1Aff* __restrict__ bases, uint32
   const G1Aff a = load_aff(bases, i);
   if (err && (!a.x.is_reduced() || !a.y.is_reduced())) atomicOr(err, 1u);
   const Fq y = fq_to_r29w(a.y);
+  const r29::F x = r29::to_r29(a.x.v);
+  Fq xw;
+  r29::to_words(x, xw.v);
   uint4* o = vtab + 4 * (size_t)i;
-  st_words(o, fq_to_r29w(a.x));
+  st_words(o, xw);
   st_words(o + 2, y);
-  if (glv) {
-    Fq beta;
+  if (glv) {  // beta x in the 29-bit form directly: beta R' (GLV_BETA_MONT re-expressed, 2^261)
+    constexpr uint32_t kBeta29[r29::L] = {0xa337995u, 0x158d1d23u, 0x189c9b98u, 0x12fa4e45u, 0x185faadcu,
+                                         0x176f16du, 0xeed93bau,  0x14291140u, 0xc0afeu};
+    r29::F beta;
 #pragma unroll
-    for (int j = 0; j < 8; j++) beta.v[j] = GLV_BETA_MONT[j];
+    for (int j = 0; j < r29::L; j++) beta.v[j] = kBeta29[j];
+    Fq bw;
+    r29::to_words(r29::mul(x, beta), bw.v);  // below 2p
     uint4* q = vtab + 4 * ((size_t)nsplit + i);
-    st_words(q, fq_to_r29w(a.x * beta));
+    st_words(q, bw);
     st_words(q + 2, y);
   }
 }
@@ -1722,7 +1729,10 @@ static std::vector<size_t> piece_bounds(size_t n, int pieces, const std::vector<
     } else if (n >= (size_t(1) << 18) && !dflt.empty()) {
       wts = dflt;
     } else if (n >= (size_t(1) << 18)) {
-      wts = {1, 1, 1, 1};
+      // decreasing: the copy (1.7 ns per point) outpaces the pieces' accumulates (~1.3 ns), so the
+      // last piece -- whose accumulate is the call's tail -- is the smallest (round 4, 2^20, three
+      // A/B pairs: 5,4,4,3 2.594-2.597 ms vs 4 equal 2.639-2.657; 5,4,4,2,1 2.669-2.670)
+      wts = {5, 4, 4, 3};
     } else if (n >= (size_t(1) << 15)) {
       wts = {1, 1};
     } else {
@@ -1981,6 +1991,10 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
     // copy engine idle ~30 us per burst, rocprof trace); this thread queues a piece's sort /
     // accumulate as soon as the feeder has recorded the piece's events.  staged = stages done (2k + 1: piece k's scalars, 2k + 2: its
     // bases), -1 once the feeder failed.
+    // Piece 0's scalars are staged by THIS thread, right after the helper is woken: the helper's
+    // wake-up (a condition variable, tens of us) then overlaps that first copy instead of delaying
+    // it, and the helper takes over from piece 0's bases (it spins until the scalars are issued, so
+    // the copy stream keeps the scalars-then-bases order).
     std::atomic<int> staged{0}, stop{0};
     int feed_rc = SV_OK;
     std::string feed_err;
@@ -1989,11 +2003,15 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
       // the helper thread has no SV_GUARD: an exception here (std::function / vector allocation in
       // the host pool) becomes the call's SV_ERR_DEVICE instead of std::terminate
       try {
-        for (int k = 0; k < pieces && !stop.load(std::memory_order_relaxed); k++) {
+        int st0;
+        while ((st0 = staged.load(std::memory_order_acquire)) == 0) std::this_thread::yield();
+        for (int k = 0; st0 > 0 && k < pieces && !stop.load(std::memory_order_relaxed); k++) {
           const size_t lo = pb[k], hi = pb[k + 1];
-          rc = feed->stage_scalars(lo, hi, const_cast<Fr*>(scalars) + lo, cs, ev[8 + 3 * k]);
-          if (rc != SV_OK) break;
-          staged.store(2 * k + 1, std::memory_order_release);
+          if (k > 0) {
+            rc = feed->stage_scalars(lo, hi, const_cast<Fr*>(scalars) + lo, cs, ev[8 + 3 * k]);
+            if (rc != SV_OK) break;
+            staged.store(2 * k + 1, std::memory_order_release);
+          }
           rc = feed->stage_bases(lo, hi, const_cast<G1Aff*>(bases) + lo, cs, ev[9 + 3 * k]);
           if (rc != SV_OK) break;
           staged.store(2 * k + 2, std::memory_order_release);
@@ -2019,6 +2037,16 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
         ws->wait_helper();
       }
     } join{ws, stop};
+    {
+      const int rc0 = feed->stage_scalars(pb[0], pb[1], const_cast<Fr*>(scalars) + pb[0], cs, ev[8]);
+      if (rc0 != SV_OK) {
+        feed_rc = rc0;
+        feed_err = sv::last_error();
+        staged.store(-1, std::memory_order_release);  // the helper, spinning on it, exits
+        return rc0;
+      }
+      staged.store(1, std::memory_order_release);
+    }
     auto wait_stage = [&](int v) -> int {
       int x;
       while ((x = staged.load(std::memory_order_acquire)) >= 0 && x < v) std::this_thread::yield();

@@ -1,18 +1,23 @@
-// BN254 Fq over 9 x 29-bit limbs (round 4): the bucket accumulation's field.
+// BN254 Fq and Fr over 9 x 29-bit limbs (round 4): the bucket accumulation's field (Fq) and the
+// Poseidon permutation's (Fr).
 //
 // Why: with 29-bit limbs every partial product is below 2^58, so a Montgomery column of up to 27
 // of them (a fused two-product sum) plus the incoming carry stays below 2^63 -- each partial product
 // is ONE v_mad_u64_u32 into a 64-bit accumulator, where the 8 x 32-bit product of field.hpp needs a
 // v_addc after every v_mad_u64_u32 to keep the carry.  tools/ubench_r29.hip: 172 vs 144 G
 // products/s on the MI355X.  Additions pay instead (carries are propagated by shifts), so only the
-// product-heavy inner loop (XYZZ mixed additions, curve29.hpp) uses this form; everything it stores
-// is converted back to field.hpp's 8 x 32-bit R = 2^256 Montgomery form.
+// product-heavy loops use this form (the XYZZ mixed additions of curve29.hpp, the Poseidon rounds);
+// what leaves them is converted back to field.hpp's 8 x 32-bit R = 2^256 Montgomery form.  The
+// modulus is a type parameter (FqM29 = p, FrM29 = r; F29<M> carries it); F = F29<FqM29>.
 //
-// Representation: value * R' mod p with R' = 2^261, little-endian limbs v[0..8], each in
+// Representation (p below stands for the modulus; both are below 2^254 and above 2^253):
+// value * R' mod p with R' = 2^261, little-endian limbs v[0..8], each in
 // [0, 2^29) ("normalized"); values are LAZILY reduced -- each operation states the bound of its
 // output, always below 2^261.
 //   mul / sqr:   inputs below 12p  -> output below 2p   (12^2 p^2 / R' + p < 2p: 144 p < R' = 169.6 p)
 //   mul_sum2:    inputs below  9p  -> output below 2p   (2 * 81 p^2 / R' + p < 2p)
+//   mul_sum3:    a_i below 9p, b_i below p -> output below 2p (3 * 9 p^2 / R' + p < 2p; a column
+//                holds 27 + 9 partial products below 2^58 and the carry: below 2^64)
 //   sub<K>:      a - b + K p for b below K p -> below (bound of a) + K p
 //   csub<K>:     a below 2 K p -> below K p (one conditional subtraction of K p)
 // Host build: the same code runs on the CPU (tests/native/field29check.cpp checks every operation
@@ -32,41 +37,66 @@ namespace r29 {
 
 constexpr int L = 9;
 constexpr uint32_t MASK = (1u << 29) - 1;
-constexpr uint32_t NP = 0x4866389u;  // -p^-1 mod 2^29
 
-// k p, normalized 29-bit limbs (k = 1, 2, 4, 6)
-SV29_HD constexpr uint32_t kp(int k, int i) {
-  constexpr uint32_t P1[9] = {0x187cfd47u, 0x10460b6u, 0x1c72a34fu, 0x2d522d0u, 0x1585d978u,
-                              0x2db40c0u,  0x0a6e141u, 0xe5c2634u,  0x030644eu};
-  constexpr uint32_t P2[9] = {0x10f9fa8eu, 0x208c16du, 0x18e5469eu, 0x5aa45a1u, 0xb0bb2f0u,
-                              0x5b68181u,  0x14dc282u, 0x1cb84c68u, 0x060c89cu};
-  constexpr uint32_t P4[9] = {0x1f3f51cu, 0x41182dbu, 0x11ca8d3cu, 0xb548b43u, 0x161765e0u,
-                              0xb6d0302u, 0x29b8504u, 0x197098d0u, 0x0c19139u};
-  constexpr uint32_t P6[9] = {0x12edefaau, 0x61a4448u, 0xaafd3dau, 0x10fed0e5u, 0x12318d0u,
-                              0x11238484u, 0x3e94786u, 0x1628e538u, 0x12259d6u};
-  return k == 1 ? P1[i] : (k == 2 ? P2[i] : (k == 4 ? P4[i] : P6[i]));
-}
-struct F {
-  uint32_t v[L];
+// the moduli: k * modulus as normalized 29-bit limbs (k = 0..8) and -modulus^-1 mod 2^29
+struct FqM29 {  // p
+  static constexpr uint32_t NP = 0x4866389u;
+  SV29_HD static constexpr uint32_t kp(int k, int i) {
+    constexpr uint32_t T[9][9] = {
+        {0, 0, 0, 0, 0, 0, 0, 0, 0},
+        {0x187cfd47u, 0x10460b6u, 0x1c72a34fu, 0x2d522d0u, 0x1585d978u, 0x2db40c0u, 0xa6e141u, 0xe5c2634u, 0x30644eu},
+        {0x10f9fa8eu, 0x208c16du, 0x18e5469eu, 0x5aa45a1u, 0xb0bb2f0u, 0x5b68181u, 0x14dc282u, 0x1cb84c68u, 0x60c89cu},
+        {0x976f7d5u, 0x30d2224u, 0x1557e9edu, 0x87f6872u, 0x918c68u, 0x891c242u, 0x1f4a3c3u, 0xb14729cu, 0x912cebu},
+        {0x1f3f51cu, 0x41182dbu, 0x11ca8d3cu, 0xb548b43u, 0x161765e0u, 0xb6d0302u, 0x29b8504u, 0x197098d0u, 0xc19139u},
+        {0x1a70f263u, 0x515e391u, 0xe3d308bu, 0xe29ae14u, 0xb9d3f58u, 0xe4843c3u, 0x3426645u, 0x7ccbf04u, 0xf1f588u},
+        {0x12edefaau, 0x61a4448u, 0xaafd3dau, 0x10fed0e5u, 0x12318d0u, 0x11238484u, 0x3e94786u, 0x1628e538u, 0x12259d6u},
+        {0xb6aecf1u, 0x71ea4ffu, 0x7227729u, 0x13d3f3b6u, 0x16a8f248u, 0x13fec544u, 0x49028c7u, 0x4850b6cu, 0x152be25u},
+        {0x3e7ea38u, 0x82305b6u, 0x3951a78u, 0x16a91687u, 0xc2ecbc0u, 0x16da0605u, 0x5370a08u, 0x12e131a0u, 0x1832273u}};
+    return T[k][i];
+  }
+};
+struct FrM29 {  // r
+  static constexpr uint32_t NP = 0xfffffffu;
+  SV29_HD static constexpr uint32_t kp(int k, int i) {
+    constexpr uint32_t T[9][9] = {
+        {0, 0, 0, 0, 0, 0, 0, 0, 0},
+        {0x10000001u, 0x1f0fac9fu, 0xe5c2450u, 0x7d090f3u, 0x1585d283u, 0x2db40c0u, 0xa6e141u, 0xe5c2634u, 0x30644eu},
+        {0x2u, 0x1e1f593fu, 0x1cb848a1u, 0xfa121e6u, 0xb0ba506u, 0x5b68181u, 0x14dc282u, 0x1cb84c68u, 0x60c89cu},
+        {0x10000003u, 0x1d2f05deu, 0xb146cf2u, 0x1771b2dau, 0x917789u, 0x891c242u, 0x1f4a3c3u, 0xb14729cu, 0x912cebu},
+        {0x4u, 0x1c3eb27eu, 0x19709143u, 0x1f4243cdu, 0x16174a0cu, 0xb6d0302u, 0x29b8504u, 0x197098d0u, 0xc19139u},
+        {0x10000005u, 0x1b4e5f1du, 0x7ccb594u, 0x712d4c1u, 0xb9d1c90u, 0xe4843c3u, 0x3426645u, 0x7ccbf04u, 0xf1f588u},
+        {0x6u, 0x1a5e0bbdu, 0x1628d9e5u, 0xee365b4u, 0x122ef13u, 0x11238484u, 0x3e94786u, 0x1628e538u, 0x12259d6u},
+        {0x10000007u, 0x196db85cu, 0x484fe36u, 0x16b3f6a8u, 0x16a8c196u, 0x13fec544u, 0x49028c7u, 0x4850b6cu, 0x152be25u},
+        {0x8u, 0x187d64fcu, 0x12e12287u, 0x1e84879bu, 0xc2e9419u, 0x16da0605u, 0x5370a08u, 0x12e131a0u, 0x1832273u}};
+    return T[k][i];
+  }
 };
 
-SV29_HD F zero() {
-  F r;
+template <class M>
+struct F29 {
+  uint32_t v[L];
+};
+using F = F29<FqM29>;
+
+template <class M = FqM29>
+SV29_HD F29<M> zero() {
+  F29<M> r;
 #pragma unroll
   for (int i = 0; i < L; i++) r.v[i] = 0;
   return r;
 }
-template <int K>
-SV29_HD F kp_f() {
-  F r;
+template <int K, class M = FqM29>
+SV29_HD F29<M> kp_f() {
+  F29<M> r;
 #pragma unroll
-  for (int i = 0; i < L; i++) r.v[i] = kp(K, i);
+  for (int i = 0; i < L; i++) r.v[i] = M::kp(K, i);
   return r;
 }
 
 // 8 x 32-bit words (a value below 2^256) <-> 9 x 29-bit limbs (the value unchanged)
-SV29_HD F from_words(const uint32_t* w) {
-  F r;
+template <class M = FqM29>
+SV29_HD F29<M> from_words(const uint32_t* w) {
+  F29<M> r;
 #pragma unroll
   for (int i = 0; i < L; i++) {
     const int bit = 29 * i, j = bit >> 5, s = bit & 31;
@@ -76,7 +106,8 @@ SV29_HD F from_words(const uint32_t* w) {
   }
   return r;
 }
-SV29_HD void to_words(const F& a, uint32_t* w) {  // a below 2^256
+template <class M>
+SV29_HD void to_words(const F29<M>& a, uint32_t* w) {  // a below 2^256
 #pragma unroll
   for (int j = 0; j < 8; j++) {
     const int bit = 32 * j, i = bit / 29, s = bit % 29;
@@ -95,11 +126,11 @@ SV29_HD uint64_t mad(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * 
   {                                                                    \
     _Pragma("unroll") for (int i = 0; i < L; i++) {                    \
       const int j = (k) - i;                                           \
-      if (i < (k) && j >= 1 && j < L) acc = mad(m[i], kp(1, j), acc);  \
+      if (i < (k) && j >= 1 && j < L) acc = mad(m[i], M::kp(1, j), acc); \
     }                                                                  \
     if ((k) < L) {                                                     \
-      m[(k)] = ((uint32_t)acc * NP) & MASK;                            \
-      acc = mad(m[(k)], kp(1, 0), acc);                                \
+      m[(k)] = ((uint32_t)acc * M::NP) & MASK;                         \
+      acc = mad(m[(k)], M::kp(1, 0), acc);                             \
     } else {                                                           \
       t.v[(k) - L] = (uint32_t)acc & MASK;                             \
     }                                                                  \
@@ -107,9 +138,10 @@ SV29_HD uint64_t mad(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * 
   }
 
 // a b / R' mod p, below 2p for a, b below 12p
-SV29_HD F mul(const F& a, const F& b) {
+template <class M>
+SV29_HD F29<M> mul(const F29<M>& a, const F29<M>& b) {
   uint32_t m[L];
-  F t;
+  F29<M> t;
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 2 * L - 1; k++) {
@@ -125,9 +157,10 @@ SV29_HD F mul(const F& a, const F& b) {
 }
 
 // a^2 / R' mod p, below 2p for a below 12p: the cross products once, against 2 a_j
-SV29_HD F sqr(const F& a) {
+template <class M>
+SV29_HD F29<M> sqr(const F29<M>& a) {
   uint32_t m[L], a2[L];
-  F t;
+  F29<M> t;
 #pragma unroll
   for (int i = 0; i < L; i++) a2[i] = a.v[i] << 1;
   uint64_t acc = 0;
@@ -147,9 +180,10 @@ SV29_HD F sqr(const F& a) {
 
 // (a0 b0 + a1 b1) / R' mod p with ONE reduction, below 2p for inputs below 9p (a column: at most
 // 27 products below 2^58 plus the carry, below 2^63)
-SV29_HD F mul_sum2(const F& a0, const F& b0, const F& a1, const F& b1) {
+template <class M>
+SV29_HD F29<M> mul_sum2(const F29<M>& a0, const F29<M>& b0, const F29<M>& a1, const F29<M>& b1) {
   uint32_t m[L];
-  F t;
+  F29<M> t;
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 2 * L - 1; k++) {
@@ -166,16 +200,40 @@ SV29_HD F mul_sum2(const F& a0, const F& b0, const F& a1, const F& b1) {
   t.v[L - 1] = (uint32_t)acc;
   return t;
 }
+// (a0 b0 + a1 b1 + a2 b2) / R' mod p with ONE reduction, below 2p for a_i below 9p and b_i below p
+// (an MDS row over constants)
+template <class M>
+SV29_HD F29<M> mul_sum3(const F29<M>& a0, const F29<M>& b0, const F29<M>& a1, const F29<M>& b1,
+                        const F29<M>& a2, const F29<M>& b2) {
+  uint32_t m[L];
+  F29<M> t;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * L - 1; k++) {
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < L) {
+        acc = mad(a0.v[i], b0.v[j], acc);
+        acc = mad(a1.v[i], b1.v[j], acc);
+        acc = mad(a2.v[i], b2.v[j], acc);
+      }
+    }
+    SV29_REDUCE_COLUMN(k)
+  }
+  t.v[L - 1] = (uint32_t)acc;
+  return t;
+}
 #undef SV29_REDUCE_COLUMN
 
 // a - b + K p, normalized (b below K p; the result is below bound(a) + K p)
-template <int K>
-SV29_HD F sub(const F& a, const F& b) {
-  F r;
+template <int K, class M>
+SV29_HD F29<M> sub(const F29<M>& a, const F29<M>& b) {
+  F29<M> r;
   int32_t c = 0;
 #pragma unroll
   for (int i = 0; i < L; i++) {
-    const int32_t x = (int32_t)(a.v[i] + kp(K, i)) - (int32_t)b.v[i] + c;
+    const int32_t x = (int32_t)(a.v[i] + M::kp(K, i)) - (int32_t)b.v[i] + c;
     c = x >> 29;  // arithmetic: floor division by 2^29 (-1, 0 or 1)
     r.v[i] = (uint32_t)x & MASK;
   }
@@ -183,8 +241,9 @@ SV29_HD F sub(const F& a, const F& b) {
 }
 
 // a + b, normalized (below bound(a) + bound(b), which must stay below 2^261)
-SV29_HD F add(const F& a, const F& b) {
-  F r;
+template <class M>
+SV29_HD F29<M> add(const F29<M>& a, const F29<M>& b) {
+  F29<M> r;
   uint32_t c = 0;
 #pragma unroll
   for (int i = 0; i < L; i++) {
@@ -196,34 +255,37 @@ SV29_HD F add(const F& a, const F& b) {
 }
 
 // a below 2 K p -> below K p: a - K p when that does not go negative
-template <int K>
-SV29_HD F csub(const F& a) {
-  F d;
+template <int K, class M>
+SV29_HD F29<M> csub(const F29<M>& a) {
+  F29<M> d;
   int32_t c = 0;
 #pragma unroll
   for (int i = 0; i < L; i++) {
-    const int32_t x = (int32_t)a.v[i] - (int32_t)kp(K, i) + c;
+    const int32_t x = (int32_t)a.v[i] - (int32_t)M::kp(K, i) + c;
     c = x >> 29;
     d.v[i] = (uint32_t)x & MASK;
   }
   return c < 0 ? a : d;
 }
 
-SV29_HD bool eq(const F& a, const F& b) {
+template <class M>
+SV29_HD bool eq(const F29<M>& a, const F29<M>& b) {
   uint32_t x = 0;
 #pragma unroll
   for (int i = 0; i < L; i++) x |= a.v[i] ^ b.v[i];
   return x == 0;
 }
-SV29_HD bool is_zero(const F& a) {
+template <class M>
+SV29_HD bool is_zero(const F29<M>& a) {
   uint32_t x = 0;
 #pragma unroll
   for (int i = 0; i < L; i++) x |= a.v[i];
   return x == 0;
 }
 
-// a == 0 mod p for a below 6p: a in {0, p, .., 5p}.  The low limb filters (a match of limb 0 with
-// one of the six multiples is needed), so the full comparisons run only on that rare path.
+// a == 0 mod p for a below 6p: a in {0, p, .., 5p} (Fq only: LOW holds p's multiples).  The low
+// limb filters (a match of limb 0 with one of the six multiples is needed), so the full comparisons
+// run only on that rare path.
 SV29_HD bool is_zero_mod_p_6p(const F& a) {
   constexpr uint32_t LOW[6] = {0u, 0x187cfd47u, 0x10f9fa8eu, 0x976f7d5u, 0x1f3f51cu, 0x1a70f263u};
   bool cand = false;
@@ -237,8 +299,9 @@ SV29_HD bool is_zero_mod_p_6p(const F& a) {
 // Form changes without a product: x R' = 32 (x R) mod p, so the way in is a 5-bit shift and a
 // small reduction, the way out an exact division by 32 (a Montgomery reduction by 2^5).
 // x R (field.hpp's 8 x 32-bit form, below p) -> x R', below 2p
-SV29_HD F to_r29(const uint32_t* w) {
-  F r;
+template <class M = FqM29>
+SV29_HD F29<M> to_r29(const uint32_t* w) {
+  F29<M> r;
 #pragma unroll
   for (int i = 0; i < L; i++) {  // limb i = bits [29 i - 5, 29 i + 24) of the value
     if (i == 0) {
@@ -252,28 +315,29 @@ SV29_HD F to_r29(const uint32_t* w) {
   }
   // r = 32 x R < 32 p: subtract q p, q = floor(r8 / (p8 + 1)) from the top limbs (a multiply-high
   // by floor(2^32 / (p8 + 1))); q is at most 2 below floor(r / p), so the rest is below 3p
-  const uint32_t q = (uint32_t)(((uint64_t)r.v[L - 1] * (0xffffffffull / (kp(1, L - 1) + 1))) >> 32);
+  const uint32_t q = (uint32_t)(((uint64_t)r.v[L - 1] * (0xffffffffull / (M::kp(1, L - 1) + 1))) >> 32);
   int64_t c = 0;
 #pragma unroll
   for (int i = 0; i < L; i++) {
-    const int64_t x = (int64_t)r.v[i] - (int64_t)q * kp(1, i) + c;
+    const int64_t x = (int64_t)r.v[i] - (int64_t)q * M::kp(1, i) + c;
     c = x >> 29;
     r.v[i] = (uint32_t)x & MASK;
   }
   return csub<2>(r);
 }
 // x R' (below 4p) -> x R canonical (below p), as 8 x 32-bit words
-SV29_HD void to_r32(const F& a, uint32_t* w) {
-  const uint32_t m = (a.v[0] * NP) & 31;  // a + m p = 0 mod 32
-  F t;
+template <class M>
+SV29_HD void to_r32(const F29<M>& a, uint32_t* w) {
+  const uint32_t m = (a.v[0] * M::NP) & 31;  // a + m p = 0 mod 32
+  F29<M> t;
   uint64_t c = 0;
 #pragma unroll
   for (int i = 0; i < L; i++) {
-    c += (uint64_t)m * kp(1, i) + a.v[i];
+    c += (uint64_t)m * M::kp(1, i) + a.v[i];
     t.v[i] = (uint32_t)c & MASK;
     c >>= 29;
   }
-  F d;  // (a + m p) / 32, below a / 32 + p < 2p
+  F29<M> d;  // (a + m p) / 32, below a / 32 + p < 2p
 #pragma unroll
   for (int i = 0; i < L; i++) d.v[i] = (t.v[i] >> 5) | ((i + 1 < L ? t.v[i + 1] : (uint32_t)c) << 24 & MASK);
   to_words(csub<1>(d), w);

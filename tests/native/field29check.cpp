@@ -6,6 +6,7 @@
 #include <cstring>
 #include <initializer_list>
 #include <string>
+#include <type_traits>
 
 #include "curve29.hpp"
 
@@ -21,21 +22,23 @@ static uint64_t rnd() {
   return s;
 }
 // a value below k p: random limbs, then csub down (k p below 2^261), or a boundary value
-static F below(int k, int mode) {
-  F r;
-  if (mode == 1) return zero();
+template <class M>
+static F29<M> below(int k, int mode) {
+  F29<M> r;
+  if (mode == 1) return zero<M>();
   if (mode == 2) {  // k p - 1
-    F kp1 = k == 1 ? kp_f<1>() : k == 2 ? kp_f<2>() : k == 4 ? kp_f<4>() : kp_f<6>();
-    F one = zero();
+    F29<M> kp1 = k == 1 ? kp_f<1, M>() : k == 2 ? kp_f<2, M>() : k == 4 ? kp_f<4, M>() : kp_f<6, M>();
+    F29<M> one = zero<M>();
     one.v[0] = 1;
-    F t = sub<1>(kp1, one);  // kp - 1 + p
+    F29<M> t = sub<1>(kp1, one);  // kp - 1 + p
     return csub<1>(t) /* value kp - 1 when k >= 1 */;
   }
   for (int i = 0; i < L; i++) r.v[i] = (uint32_t)rnd() & MASK;
   r.v[L - 1] &= (n_top_bits() == 23 ? 0x7fffffu : 0x3fffffu);  // below 2^255 (~4.4 p) or 2^254
   return r;
 }
-static void pr(const F& a) {
+template <class M>
+static void pr(const F29<M>& a) {
   printf(" ");
   for (int i = L - 1; i >= 0; i--) printf("%08x", a.v[i]);
 }
@@ -63,19 +66,24 @@ static int madd_mode() {
   return 0;
 }
 
-int main(int argc, char** argv) {
-  if (argc > 1 && !strcmp(argv[1], "madd")) return madd_mode();
+template <class M>
+static int run_ops(bool fq) {
   for (int n = 0; n < 3000; n++) {
     const int mode = n < 40 ? n % 3 : 0;
     g_top = (n & 1) ? 23 : 22;
     // raw random below 2^255 (~4.4 p); the Python side knows each op's input bound and checks it
-    F a = below(12, mode), b = below(12, (mode + 1) % 3), c = below(12, mode), d = below(12, (mode + 2) % 3);
+    F29<M> a = below<M>(12, mode), b = below<M>(12, (mode + 1) % 3), c = below<M>(12, mode), d = below<M>(12, (mode + 2) % 3);
     printf("mul");
     pr(a), pr(b), pr(mul(a, b));
     printf("\nsqr");
     pr(a), pr(sqr(a));
     printf("\nmul_sum2");
     pr(a), pr(b), pr(c), pr(d), pr(mul_sum2(a, b, c, d));
+    {  // mul_sum3 over "constants" below p (b, d reduced)
+      const F29<M> bb = csub<1>(csub<2>(csub<4>(b))), dd = csub<1>(csub<2>(csub<4>(d))), ee = csub<1>(csub<2>(csub<4>(a)));
+      printf("\nmul_sum3");
+      pr(a), pr(bb), pr(c), pr(dd), pr(d), pr(ee), pr(mul_sum3(a, bb, c, dd, d, ee));
+    }
     printf("\nadd");
     pr(a), pr(b), pr(add(a, b));
     printf("\nsub2");
@@ -90,29 +98,31 @@ int main(int argc, char** argv) {
     pr(a), pr(csub<2>(a));
     printf("\ncsub4");
     pr(a), pr(csub<4>(a));
-    printf("\nzero6 ");
-    pr(a);
-    printf(" %d", is_zero_mod_p_6p(a) ? 1 : 0);
+    if constexpr (std::is_same<M, FqM29>::value) {
+      printf("\nzero6 ");
+      pr(a);
+      printf(" %d", is_zero_mod_p_6p(a) ? 1 : 0);
+    }
     uint32_t w[8], w2[8];
     to_words(a, w);
-    F back = from_words(w);
+    F29<M> back = from_words<M>(w);
     printf("\nwords");
     pr(a), pr(back);
     // conversions (inputs below p as 8 x 32 words: a mod p computed via csub chain)
-    F ar = csub<1>(csub<2>(csub<4>(a)));
+    F29<M> ar = csub<1>(csub<2>(csub<4>(a)));
     to_words(ar, w);
-    F r29 = to_r29(w);
+    F29<M> r29 = to_r29<M>(w);
     to_r32(r29, w2);
     printf("\nto_r29");
-    pr(ar), pr(r29), pr(from_words(w2));
-    F a4 = csub<4>(a);  // below 4p when a is below 8p
+    pr(ar), pr(r29), pr(from_words<M>(w2));
+    F29<M> a4 = csub<4>(a);  // below 4p when a is below 8p
     to_r32(a4, w2);
     printf("\nto_r32");
-    pr(a4), pr(from_words(w2));
+    pr(a4), pr(from_words<M>(w2));
     printf("\n");
   }
   // zero tests on exact multiples of p
-  for (int k = 0; k < 6; k++) {
+  for (int k = 0; fq && k < 6; k++) {
     F m = zero();
     for (int j = 0; j < k; j++) m = sub<1>(m, zero());  // m + p
     printf("zero6 ");
@@ -121,3 +131,10 @@ int main(int argc, char** argv) {
   }
   return 0;
 }
+
+int main(int argc, char** argv) {
+  if (argc > 1 && !strcmp(argv[1], "madd")) return madd_mode();
+  const bool fr = argc > 1 && !strcmp(argv[1], "fr");  // the same checks over Fr (FrM29)
+  return fr ? run_ops<FrM29>(false) : run_ops<FqM29>(true);
+}
+

@@ -32,14 +32,25 @@ def _limbs(h):
     return sum(int(h[8 * i:8 * i + 8], 16) << (29 * (8 - i)) for i in range(9))
 
 
-def test_field_ops_values_and_bounds(f29):
-    out = subprocess.run([f29], capture_output=True, text=True, check=True).stdout
+@pytest.mark.parametrize("field", ["fq", "fr"])
+def test_field_ops_values_and_bounds(f29, field):
+    """Every operation over both moduli (FqM29 = p for the bucket chain, FrM29 = r for Poseidon)."""
+    P = ob.P if field == "fq" else ob.R  # noqa: N806 (the modulus of this run)
+    RINV = pow((1 << 261) % P, -1, P)  # noqa: N806
+    args = [f29] if field == "fq" else [f29, "fr"]
+    out = subprocess.run(args, capture_output=True, text=True, check=True).stdout
     counts = {}
     for line in out.splitlines():
         f = line.split()
         op, v = f[0], [_limbs(x) for x in f[1:]]
         counts[op] = counts.get(op, 0) + 1
-        if op in ("mul", "sqr", "mul_sum2"):
+        if op == "mul_sum3":
+            a0, b0, a1, b1, a2, b2, r = v
+            if any(x >= 9 * P for x in (a0, a1, a2)) or any(x >= P for x in (b0, b1, b2)):
+                continue
+            assert r < 2 * P, line
+            assert r % P == (a0 * b0 + a1 * b1 + a2 * b2) * RINV % P, line
+        elif op in ("mul", "sqr", "mul_sum2"):
             bound_in = 12 * P if op != "mul_sum2" else 9 * P
             ins, r = v[:-1], v[-1]
             if any(x >= bound_in for x in ins):
@@ -82,7 +93,8 @@ def test_field_ops_values_and_bounds(f29):
         elif op == "to_r32":
             a, r = v
             assert r < P and r == a * pow(32, -1, P) % P, line
-    assert counts.get("mul", 0) >= 3000 and counts.get("zero6", 0) >= 3006 and counts.get("to_r32", 0) >= 3000
+    assert counts.get("mul", 0) >= 3000 and counts.get("to_r32", 0) >= 3000 and counts.get("mul_sum3", 0) >= 3000
+    assert counts.get("zero6", 0) >= (3006 if field == "fq" else 0)
 
 
 def _state(pt, rng, identity=False):

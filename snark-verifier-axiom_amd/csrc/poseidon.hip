@@ -13,7 +13,10 @@
 // lane's state stays in VGPRs.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "field.hpp"
+#include "field29.hpp"
 #include "poseidon.hpp"
 #include "poseidon_consts.hpp"
 #include "runtime.hpp"
@@ -26,6 +29,12 @@ __constant__ uint32_t c_end3[] = SV_POSEIDON_T3_END_INIT;
 __constant__ uint32_t c_mds3[] = SV_POSEIDON_T3_MDS_INIT;
 __constant__ uint32_t c_pre3[] = SV_POSEIDON_T3_PRE_INIT;
 __constant__ uint32_t c_sparse3[] = SV_POSEIDON_T3_SPARSE_INIT;
+__constant__ uint32_t c_start3_29[] = SV_POSEIDON_T3_START_R29_INIT;
+__constant__ uint32_t c_partial3_29[] = SV_POSEIDON_T3_PARTIAL_R29_INIT;
+__constant__ uint32_t c_end3_29[] = SV_POSEIDON_T3_END_R29_INIT;
+__constant__ uint32_t c_mds3_29[] = SV_POSEIDON_T3_MDS_R29_INIT;
+__constant__ uint32_t c_pre3_29[] = SV_POSEIDON_T3_PRE_R29_INIT;
+__constant__ uint32_t c_sparse3_29[] = SV_POSEIDON_T3_SPARSE_R29_INIT;
 __constant__ uint32_t c_start5[] = SV_POSEIDON_T5_START_INIT;
 __constant__ uint32_t c_partial5[] = SV_POSEIDON_T5_PARTIAL_INIT;
 __constant__ uint32_t c_end5[] = SV_POSEIDON_T5_END_INIT;
@@ -144,6 +153,78 @@ __device__ __forceinline__ void permute(Fr (&s)[T]) {
   for (int i = 0; i < T; i++) s[i] = fe_canon2p(s[i]);
 }
 
+// ---- t = 3 over field29.hpp's 9 x 29-bit limbs (round 4, default; SVGPU_POSEIDON_R29=0 keeps the
+// 8 x 32-bit rounds above).  Every partial product is one v_mad_u64_u32 with no carry add, and an
+// MDS row is ONE Montgomery reduction of three products (mul_sum3).  Same schedule, constants in
+// the limb form (c 2^261 mod r, tools/gen_consts.py); the state enters and leaves in field.hpp's
+// form.  Bounds (field29.hpp's contract, r the modulus):
+//   * pow5 of a word below 12 r is below 2 r; "+ constant" makes it below 3 r (no reduction);
+//   * an MDS row of words below 9 r with constants below r is below 2 r;
+//   * a partial round's state[i] += col_hat[i-1] * state[0] adds a product below 2 r to a word
+//     below 4 r and is brought back below 4 r (csub<4>: below 8 r in);
+//   * the last full round leaves words below 2 r, made canonical on the way out (to_r32).
+namespace p29 {
+using E = r29::F29<r29::FrM29>;
+__device__ __forceinline__ E ld(const uint32_t* p) {  // a constant (wave-uniform: scalar loads)
+  E r;
+#pragma unroll
+  for (int i = 0; i < r29::L; i++) r.v[i] = p[i];
+  return r;
+}
+__device__ __forceinline__ E pow5(const E& x) { return r29::mul(r29::sqr(r29::sqr(x)), x); }
+// the state as three named words (an E[3] array ended up in scratch memory)
+__device__ __forceinline__ E row(const E& a, const E& b, const E& c, const uint32_t* m) {
+  return r29::mul_sum3(a, ld(m), b, ld(m + 9), c, ld(m + 18));
+}
+__device__ __forceinline__ void mds(E& a, E& b, E& c, const uint32_t* m) {
+  const E o0 = row(a, b, c, m), o1 = row(a, b, c, m + 27), o2 = row(a, b, c, m + 54);
+  a = o0, b = o1, c = o2;
+}
+__device__ __forceinline__ void full(E& a, E& b, E& c, const uint32_t* k, const uint32_t* m) {
+  if (k) {
+    a = r29::add(pow5(a), ld(k));
+    b = r29::add(pow5(b), ld(k + 9));
+    c = r29::add(pow5(c), ld(k + 18));
+  } else {
+    a = pow5(a), b = pow5(b), c = pow5(c);
+  }
+  mds(a, b, c, m);
+}
+__device__ __forceinline__ void permute(E& a, E& b, E& c) {
+  constexpr int RF = SV_POSEIDON_T3_RF, RP = SV_POSEIDON_T3_RP, H = RF / 2;
+  a = r29::add(a, ld(c_start3_29));
+  b = r29::add(b, ld(c_start3_29 + 9));
+  c = r29::add(c, ld(c_start3_29 + 18));
+  for (int r = 1; r < H; r++) full(a, b, c, c_start3_29 + r * 27, c_mds3_29);
+  full(a, b, c, c_start3_29 + H * 27, c_pre3_29);
+  for (int r = 0; r < RP; r++) {
+    a = r29::add(pow5(a), ld(c_partial3_29 + r * 9));
+    const uint32_t* rw = c_sparse3_29 + r * 5 * 9;
+    const E a2 = row(a, b, c, rw);
+    b = r29::csub<4>(r29::add(b, r29::mul(a, ld(rw + 27))));
+    c = r29::csub<4>(r29::add(c, r29::mul(a, ld(rw + 36))));
+    a = a2;
+  }
+  for (int r = 0; r < H - 1; r++) full(a, b, c, c_end3_29 + r * 27, c_mds3_29);
+  full(a, b, c, nullptr, c_mds3_29);
+}
+}  // namespace p29
+
+// the permutation on field.hpp words (Montgomery, reduced): the 29-bit rounds for t = 3 when R29
+template <int T, bool R29>
+__device__ __forceinline__ void permute_sel(Fr (&s)[T]) {
+  if constexpr (R29 && T == 3) {
+    p29::E a = r29::to_r29<r29::FrM29>(s[0].v), b = r29::to_r29<r29::FrM29>(s[1].v),
+           c = r29::to_r29<r29::FrM29>(s[2].v);
+    p29::permute(a, b, c);
+    r29::to_r32(a, s[0].v);
+    r29::to_r32(b, s[1].v);
+    r29::to_r32(c, s[2].v);
+  } else {
+    permute<T>(s);
+  }
+}
+
 __device__ __forceinline__ Fr load_fr(const Fr* p, int mont) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
   const uint4 a = q[0], b = q[1];
@@ -160,14 +241,14 @@ __device__ __forceinline__ void store_fr(Fr* p, Fr v, int mont) {
   q[1] = make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]);
 }
 
-template <int T>
+template <int T, bool R29>
 __global__ void __launch_bounds__(256) k_poseidon_permute(Fr* __restrict__ st, uint32_t n, int mont) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   Fr s[T];
 #pragma unroll
   for (int k = 0; k < T; k++) s[k] = load_fr(st + (size_t)i * T + k, mont);
-  permute<T>(s);
+  permute_sel<T, R29>(s);
 #pragma unroll
   for (int k = 0; k < T; k++) store_fr(st + (size_t)i * T + k, s[k], mont);
 }
@@ -179,7 +260,7 @@ __global__ void __launch_bounds__(256) k_poseidon_permute(Fr* __restrict__ st, u
 // and the state is permuted; when the buffer length is a multiple of RATE (including 0) one more
 // permutation runs on the padded empty chunk.  The challenge is state[1].  Elements must be reduced
 // field elements (halo2curves' Fr always is; the Python mirror reduces its ints mod r).
-template <int T>
+template <int T, bool R29>
 __global__ void __launch_bounds__(256) k_poseidon_squeeze(Fr* __restrict__ st, const Fr* __restrict__ el,
                                                          const uint64_t* __restrict__ off, uint32_t n, int mont,
                                                          Fr* __restrict__ out) {
@@ -198,16 +279,22 @@ __global__ void __launch_bounds__(256) k_poseidon_squeeze(Fr* __restrict__ st, c
       if ((uint64_t)k < m) s[k + 1] = s[k + 1] + load_fr(el + p + k, mont);
       if ((uint64_t)k == m) s[k + 1] = s[k + 1] + Fr::one();  // 10* padding of a short chunk
     }
-    permute<T>(s);
+    permute_sel<T, R29>(s);
     p += m;
   }
   if ((e - b) % RATE == 0) {  // exact: one more permutation of the padded empty chunk
     s[1] = s[1] + Fr::one();
-    permute<T>(s);
+    permute_sel<T, R29>(s);
   }
 #pragma unroll
   for (int k = 0; k < T; k++) store_fr(st + (size_t)j * T + k, s[k], mont);
   if (out) store_fr(out + j, s[1], mont);
+}
+
+// t = 3 on the 29-bit limbs unless SVGPU_POSEIDON_R29=0 (read per call)
+static bool poseidon_r29() {
+  const char* e = getenv("SVGPU_POSEIDON_R29");
+  return !e || atoi(e) != 0;
 }
 
 int poseidon_permute_device(void* d_states, size_t n, int t, int form, hipStream_t st) {
@@ -218,10 +305,15 @@ int poseidon_permute_device(void* d_states, size_t n, int t, int form, hipStream
   }
   const uint32_t blocks = (uint32_t)((n + 255) / 256);
   Fr* s = static_cast<Fr*>(d_states);
-  if (t == 3)
-    hipLaunchKernelGGL(k_poseidon_permute<3>, dim3(blocks), dim3(256), 0, st, s, (uint32_t)n, form);
+  if (t == 3 && poseidon_r29())
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_poseidon_permute<3, true>), dim3(blocks), dim3(256), 0, st, s, (uint32_t)n,
+                       form);
+  else if (t == 3)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_poseidon_permute<3, false>), dim3(blocks), dim3(256), 0, st, s, (uint32_t)n,
+                       form);
   else if (t == 5)
-    hipLaunchKernelGGL(k_poseidon_permute<5>, dim3(blocks), dim3(256), 0, st, s, (uint32_t)n, form);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_poseidon_permute<5, false>), dim3(blocks), dim3(256), 0, st, s, (uint32_t)n,
+                       form);
   else {
     set_error("poseidon: unsupported width t = %d (3 or 5)", t);
     return SV_ERR_ARG;
@@ -241,10 +333,15 @@ int poseidon_squeeze_device(void* d_states, const void* d_elements, const uint64
   Fr* s = static_cast<Fr*>(d_states);
   const Fr* e = static_cast<const Fr*>(d_elements);
   Fr* o = static_cast<Fr*>(d_out);
-  if (t == 3)
-    hipLaunchKernelGGL(k_poseidon_squeeze<3>, dim3(blocks), dim3(256), 0, st, s, e, d_offsets, (uint32_t)n, form, o);
+  if (t == 3 && poseidon_r29())
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_poseidon_squeeze<3, true>), dim3(blocks), dim3(256), 0, st, s, e, d_offsets,
+                       (uint32_t)n, form, o);
+  else if (t == 3)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_poseidon_squeeze<3, false>), dim3(blocks), dim3(256), 0, st, s, e, d_offsets,
+                       (uint32_t)n, form, o);
   else if (t == 5)
-    hipLaunchKernelGGL(k_poseidon_squeeze<5>, dim3(blocks), dim3(256), 0, st, s, e, d_offsets, (uint32_t)n, form, o);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_poseidon_squeeze<5, false>), dim3(blocks), dim3(256), 0, st, s, e, d_offsets,
+                       (uint32_t)n, form, o);
   else {
     set_error("poseidon: unsupported width t = %d (3 or 5)", t);
     return SV_ERR_ARG;

@@ -53,5 +53,30 @@ SV29_HD Xyzz madd(const Xyzz& p, const F& x2, const F& y2) {
   return {X3, Y3, mul(ZZ, PP), mul(ZZZ, PPP)};
 }
 
+// p + q, both XYZZ states (bounds as above; either may be the identity).  add-2008-s; the
+// doubling case (p = q) runs through the same products as in madd: dbl-2008-s-1's U = 2Y, M = 3X²,
+// S = X V, ZZ3 = V ZZ, ZZZ3 = W ZZZ are the addition's Pd, Rd, Q, ZZ3, ZZZ3 with U1 = X, S1 = Y and
+// q's ZZ, ZZZ taken as 1, and no PPP term in X3.
+SV29_HD Xyzz add(const Xyzz& p, const Xyzz& q) {
+  if (is_identity(p)) return q;
+  if (is_identity(q)) return p;
+  F U1 = mul(p.X, q.ZZ), S1 = mul(p.Y, q.ZZZ);                  // < 2p
+  F Pd = sub<2>(mul(q.X, p.ZZ), U1), Rd = sub<2>(mul(q.Y, p.ZZZ), S1);  // < 4p
+  F qZZ = q.ZZ, qZZZ = q.ZZZ;
+  bool dbl = false;
+  if (is_zero_mod_p_6p(Pd)) {
+    if (!is_zero_mod_p_6p(Rd)) return identity();
+    const F x2 = sqr(p.X);
+    Pd = add(p.Y, p.Y);          // < 4p
+    Rd = add(add(x2, x2), x2);   // < 6p
+    U1 = p.X, S1 = p.Y, qZZ = one(), qZZZ = one();
+    dbl = true;
+  }
+  const F PP = sqr(Pd), PPP = mul(Pd, PP), Q = mul(U1, PP), R2 = sqr(Rd);  // < 2p (U1 < 4p)
+  const F X3 = csub<4>(sub<4>(dbl ? R2 : sub<2>(R2, PPP), add(Q, Q)));
+  const F Y3 = mul_sum2(Rd, sub<4>(Q, X3), S1, sub<2>(zero(), PPP));
+  return {X3, Y3, mul(mul(p.ZZ, qZZ), PP), mul(mul(p.ZZZ, qZZZ), PPP)};
+}
+
 }  // namespace r29
 }  // namespace sv

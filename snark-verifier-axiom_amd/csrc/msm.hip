@@ -845,6 +845,14 @@ struct AccChain<true> {
     r29::to_words(a.ZZZ, r.ZZZ.v);
     return r;
   }
+  __device__ static G1Xyzz canonical(const T& a) {  // field.hpp's canonical x R form
+    G1Xyzz r;
+    r29::to_r32(a.X, r.X.v);
+    r29::to_r32(a.Y, r.Y.v);
+    r29::to_r32(a.ZZ, r.ZZ.v);
+    r29::to_r32(a.ZZZ, r.ZZZ.v);
+    return r;
+  }
   __device__ static T madd(const T& acc, const G1Aff& p, bool neg) {
     const r29::F x = r29::from_words(p.x.v), y = r29::from_words(p.y.v);  // the table's x R' words
     return r29::madd(acc, x, neg ? r29::sub<2>(r29::zero(), y) : y);
@@ -1033,6 +1041,14 @@ __device__ __forceinline__ bool bucket_at(const G1Xyzz* __restrict__ x, const ui
                                           G1Xyzz& out, int r29w) {  // r29w: sums in the 29-bit chain's form
   if (gs && gs[i] == gs[i + 1]) return false;
   out = load_bucket(x, i, r29w);
+  return true;
+}
+
+// bucket i in the 29-bit chain's own form (r29w words -> limbs, no conversion); false when empty
+__device__ __forceinline__ bool bucket_at29(const G1Xyzz* __restrict__ x, const uint32_t* __restrict__ gs, uint32_t i,
+                                            r29::Xyzz& out) {
+  if (gs && gs[i] == gs[i + 1]) return false;
+  out = AccChain<true>::in(load_xyzz(x, i));
   return true;
 }
 
@@ -1285,7 +1301,7 @@ __device__ __forceinline__ uint32_t* tr_task(uint32_t tau, uint32_t np, uint32_t
 // -- no running sums and no A row (A = the total), a quarter of the LDS, so four blocks share a CU
 // and one block's latency-bound upper levels overlap another's wide lower ones; its wide levels
 // 1 and 2 run as whole additions (one per lane), the rest in quad form.
-template <bool RUN>
+template <bool RUN, bool R29 = false>
 __global__ void __launch_bounds__(kTreeN) k_wsum_tree(const G1Xyzz* __restrict__ X, const uint32_t* __restrict__ gst,
                                                        uint32_t N, uint32_t J, uint32_t L,
                                                        G1Xyzz* __restrict__ blk_out, int r29w) {
@@ -1302,7 +1318,30 @@ __global__ void __launch_bounds__(kTreeN) k_wsum_tree(const G1Xyzz* __restrict__
     // running sums over segment j of window g, exactly as k_wsum with base 1
     const uint32_t lo = j * L, hi = min(N, lo + L);
     G1Xyzz run = G1Xyzz::identity(), acc = G1Xyzz::identity();
-    if (hi > lo) {
+    if constexpr (R29) {
+      // the 29-bit chain's sums (r29w) read as they are stored, the running sums in the same form
+      // (r29::add: no carry adds, no per-bucket conversion), converted once for the tree below
+      r29::Xyzz run29 = r29::identity(), acc29 = r29::identity();
+      if (hi > lo) {
+        uint32_t i = hi - 1;
+        r29::Xyzz nx = r29::identity();
+        bool ne = bucket_at29(x, gs, i, nx);
+        for (;;) {
+          const r29::Xyzz cur = nx;
+          const bool cne = ne;
+          const uint32_t ci = i;
+          if (ci > lo) {
+            i = ci - 1;
+            ne = bucket_at29(x, gs, i, nx);
+          }
+          if (cne) run29 = r29::add(run29, cur);
+          acc29 = r29::add(acc29, run29);
+          if (ci == lo) break;
+        }
+      }
+      run = AccChain<true>::canonical(run29);
+      acc = AccChain<true>::canonical(acc29);
+    } else if (hi > lo) {
       uint32_t i = hi - 1;
       G1Xyzz nx = G1Xyzz::identity();
       bool ne = bucket_at(x, gs, i, nx, r29w);
@@ -2108,17 +2147,21 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   if (group_tree) {
     static thread_local int tree_attr_dev = -1;  // the > 64 KiB dynamic-LDS opt-in, once per thread/device
     if (tree_attr_dev != device) {
-      SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wsum_tree<true>),
+      SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wsum_tree<true, false>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)(2 * kTreeRow)));
+      SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wsum_tree<true, true>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)(2 * kTreeRow)));
       tree_attr_dev = device;
     }
     // windows [w0, w0 + nw) of the bucket sums xb (starts gs: empty buckets skipped) -> ping rows
+    // running sums on the 29-bit chain when the bucket sums are stored in its form
+    auto tree_run = p.r29 ? k_wsum_tree<true, true> : k_wsum_tree<true, false>;
     auto reduce_windows = [&](const G1Xyzz* xb, const uint32_t* gs, uint32_t w0, uint32_t nw) {
       if (p.tree == 2)
         hipLaunchKernelGGL(k_wsum_tree<false>, dim3(p.J / kTreeN * nw), dim3(kTreeN), kTreeRow, st, xb, gs, p.B,
                            p.J, 1u, tree_out, p.r29);
       else
-        hipLaunchKernelGGL(k_wsum_tree<true>, dim3(p.J / kTreeN * nw), dim3(kTreeN), 2 * kTreeRow, st, xb, gs,
+        hipLaunchKernelGGL(tree_run, dim3(p.J / kTreeN * nw), dim3(kTreeN), 2 * kTreeRow, st, xb, gs,
                            p.B, p.J, 1u << p.logL, tree_out, p.r29);
       hipLaunchKernelGGL(k_group_fin, dim3(nw * p.NG), dim3(128), 0, st, tree_out, p.J / kTreeN, p.NG,
                          p.tree == 2 ? 1u : 0u, ping + (size_t)w0 * p.NG);

@@ -132,8 +132,22 @@ static int run_ops(bool fq) {
   return 0;
 }
 
+// "xadd" mode: stdin lines "X Y ZZ ZZZ X' Y' ZZ' ZZZ'" (hex) -> "X3 Y3 ZZ3 ZZZ3"
+static int xadd_mode() {
+  char b[8][80];
+  while (scanf("%79s %79s %79s %79s %79s %79s %79s %79s", b[0], b[1], b[2], b[3], b[4], b[5], b[6], b[7]) == 8) {
+    const Xyzz p{parse(b[0]), parse(b[1]), parse(b[2]), parse(b[3])};
+    const Xyzz q{parse(b[4]), parse(b[5]), parse(b[6]), parse(b[7])};
+    const Xyzz r = sv::r29::add(p, q);
+    pr(r.X), pr(r.Y), pr(r.ZZ), pr(r.ZZZ);
+    printf("\n");
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "madd")) return madd_mode();
+  if (argc > 1 && !strcmp(argv[1], "xadd")) return xadd_mode();
   const bool fr = argc > 1 && !strcmp(argv[1], "fr");  // the same checks over Fr (FrM29)
   return fr ? run_ops<FrM29>(false) : run_ops<FqM29>(true);
 }

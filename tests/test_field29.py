@@ -144,3 +144,36 @@ def test_madd_group_law(f29):
         assert got == (None if want is None else tuple(want)), (st, xb, yb)
         if got is None:
             assert X == Y == ZZ == ZZZ == 0, line  # the identity is exactly zero limbs
+
+
+def test_xyzz_add_group_law(f29):
+    """The full XYZZ addition (k_wsum_tree's running sums): random representations of both points
+    within the stated bounds, the identity on either side, doubling (p = q, also in different
+    representations) and p + (-p)."""
+    rng = random.Random(31)
+    g = (1, 2)
+    cases = []
+    for n in range(300):
+        a = ob.g1_mul(g, rng.randrange(1, ob.R))
+        b = ob.g1_mul(g, rng.randrange(1, ob.R))
+        kind = n % 10
+        if kind == 6:
+            b = a
+        elif kind == 7:
+            b = ob.g1_neg(a)
+        sa = _state(a, rng, identity=(kind == 8))
+        sb = _state(b, rng, identity=(kind == 9))
+        pa = None if kind == 8 else a
+        pb = None if kind == 9 else b
+        want = pb if pa is None else (pa if pb is None else ob.g1_add(pa, pb))
+        cases.append((sa, sb, want))
+    inp = "\n".join(" ".join(hex(v) for v in (*sa, *sb)) for sa, sb, _ in cases) + "\n"
+    out = subprocess.run([f29, "xadd"], input=inp, capture_output=True, text=True, check=True).stdout.splitlines()
+    assert len(out) == len(cases)
+    for (sa, sb, want), line in zip(cases, out):
+        X, Y, ZZ, ZZZ = (_limbs(v) for v in line.split())
+        assert X < 4 * P and Y < 2 * P and ZZ < 2 * P and ZZZ < 2 * P, line
+        got = _to_affine(X, Y, ZZ, ZZZ)
+        assert got == (None if want is None else tuple(want)), (sa, sb)
+        if got is None:
+            assert X == Y == ZZ == ZZZ == 0, line

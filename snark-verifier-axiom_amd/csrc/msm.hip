@@ -807,13 +807,14 @@ __device__ __forceinline__ bool join_in_block(uint32_t gs, uint32_t ge, uint32_t
   return t1 == t0 + 1 && t0 / kBlock == t1 / kBlock;
 }
 // The accumulator of k_accumulate's chain.  R29 (default): 9 x 29-bit limbs (curve29.hpp; each
-// partial product one v_mad_u64_u32 with no carry add, 125 VGPRs = 4 waves per SIMD), points
-// converted on load (a shift + small reduction, no product).  Its bucket sums are STORED in the
+// partial product one v_mad_u64_u32 with no carry add, 125 VGPRs = 4 waves per SIMD), reading its
+// points from a table already in its form (vtab_put: a limb split per load).  Its bucket sums are STORED in the
 // chain's own Montgomery form, x R' as 8 words ("r29w": every coordinate is below 4p < 2^256), not
 // converted to field.hpp's canonical x R: a segment end runs for the whole wave whenever one of its
 // lanes ends a segment, so its work counts nearly every iteration (the conversion there cost ~70 us
 // of a 1.39 ms accumulate).  The readers convert instead: k_fixup (loads and stores r29w, so bsum
-// stays uniform for the next host-fed piece) and bucket_at (k_wsum / k_wsum_tree, once per bucket).
+// stays uniform for the next host-fed piece), bucket_at (k_wsum, k_wsum_tree<false>, once per
+// bucket), and k_wsum_tree<true, true> runs its running sums in the same form (bucket_at29).
 // SVGPU_ACC_R29=0 selects the 8 x 32-bit chain (xyzz_madd_2p_u), stored canonical.
 #ifndef SV_ACC_MADD32
 #define SV_ACC_MADD32 xyzz_madd_2p_u

@@ -1687,7 +1687,7 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
   }
   // one launch for both region kinds (SVGPU_FINE_SPLIT=1: the round-2 pair of launches, the large
   // regions optionally on a side stream)
-  static const bool fine_split = getenv("SVGPU_FINE_SPLIT") && atoi(getenv("SVGPU_FINE_SPLIT")) != 0;
+  const bool fine_split = getenv("SVGPU_FINE_SPLIT") && atoi(getenv("SVGPU_FINE_SPLIT")) != 0;  // per call
   if (!fine_split && !side) {
     hipLaunchKernelGGL(k_fine_sort<2>, dim3(nwb), dim3(1024), kFineLds, st, w.tmp, e32, w.bstart, FB, so.K, so.gst,
                        so.tstart, so.ent);
@@ -1846,7 +1846,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   // computed), and the two accumulate launches barely overlap (span 1.47 ms, their own durations
   // 1.52 ms): k_accumulate holds two 256-thread blocks per CU, so half A's 512 blocks already fill
   // the chip and half B's wait for them -- one round of blocks each, as the whole launch's two.
-  static const bool split_env = getenv("SVGPU_MSM_SPLIT") && atoi(getenv("SVGPU_MSM_SPLIT")) != 0;
+  const bool split_env = getenv("SVGPU_MSM_SPLIT") && atoi(getenv("SVGPU_MSM_SPLIT")) != 0;  // per call
   const bool split = !feed && split_env && p.W >= 2 && p.tree == 1 && n >= (size_t(1) << 16);
   const uint32_t nwh[2] = {split ? p.W / 2 : p.W, split ? p.W - p.W / 2 : 0};
   uint32_t Th[2] = {0, 0};

@@ -300,3 +300,25 @@ def test_accumulate_chains(gpu, oracle_cpp, monkeypatch, chain):
     S2 = oracle_cpp.gen_scalars(b.SEED_SCALARS, n2, start=3)
     S2[: n2 // 2] = S2[0]  # half the points in one bucket per window
     assert svgpu.msm_arrays(B2, S2, svgpu.SV_CANONICAL) == _to_pt(oracle_cpp.msm_pippenger(B2, S2, 0))
+
+
+@pytest.mark.parametrize("chain", ["1", "0"])
+@pytest.mark.parametrize("opt", ["SVGPU_MSM_SPLIT", "SVGPU_FINE_SPLIT", "SVGPU_SORT_FORK"])
+def test_optional_pipeline_paths(gpu, oracle_cpp, monkeypatch, opt, chain):
+    """The opt-in single-MSM variants kept for A/B -- window halves sorted / accumulated / reduced
+    separately (SVGPU_MSM_SPLIT: half B's sort and accumulate on the sort stream, the 29-bit point
+    table written by half A's sort only), the two-launch fine sort, the forked fine sort -- with both
+    bucket chains, against the reference Pippenger (msm.rs:238-316)."""
+    import svgpu
+    from svgpu import device as dv
+    monkeypatch.setenv(opt, "1")
+    monkeypatch.setenv("SVGPU_ACC_R29", chain)
+    for n, start in ((1 << 16, 21), (70001, 23)):
+        B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=start)
+        S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=start)
+        exp = _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
+        dev = torch.device("cuda", 0)
+        Bt = torch.from_numpy(B.view(np.int64)).to(dev)
+        St = torch.from_numpy(S.view(np.int64)).to(dev)
+        assert dv.msm(Bt, St, svgpu.SV_CANONICAL) == exp, (opt, n, "device")  # the split path's input
+        assert svgpu.msm_arrays(B, S) == exp, (opt, n, "host")

@@ -14,7 +14,8 @@
 //   k_fine_sort<2>    one block per (window, bin), both region kinds in one launch: counting sort
 //                     by the fine bucket index inside the bin's L2-resident region -> ent[], bucket
 //                     offsets gst[], owner bucket of every accumulate chunk tstart[]
-//   k_accumulate      each thread sums K consecutive sorted entries (mixed XYZZ adds; perfect
+//   k_accumulate      each thread sums K consecutive sorted entries (mixed XYZZ adds over 29-bit
+//                     limbs by default, points from a table in that form -- see AccChain; perfect
 //                     load balance whatever the digit distribution), complete buckets written
 //                     directly, bucket pieces that cross a thread boundary to pfirst/plast
 //                     (two-piece buckets inside a block are joined at the end through LDS)

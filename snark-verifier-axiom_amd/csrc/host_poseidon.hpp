@@ -139,6 +139,47 @@ inline E add_lazy(const E& a, const E& b) {
   return r;
 }
 
+// a0 b0 + a1 b1 + a2 b2 with ONE Montgomery reduction (an MDS row over constants): a_i below 2r,
+// b_i below r.  The 512-bit sum is below 6 r^2, so the reduced value is below 6 r (r / 2^256) + r
+// < 2.14 r, wrapped below 2r like add_lazy.  Two reductions fewer than three mul_lazy.
+inline E mul_sum3_lazy(const E& a0, const E& b0, const E& a1, const E& b1, const E& a2, const E& b2) {
+  uint64_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const E* as[3] = {&a0, &a1, &a2};
+  const E* bs[3] = {&b0, &b1, &b2};
+  for (int k = 0; k < 3; k++) {
+    const E& a = *as[k];
+    const E& b = *bs[k];
+    for (int i = 0; i < 4; i++) {
+      u128 c = 0;
+      for (int j = 0; j < 4; j++) {
+        const u128 s = (u128)a.l[j] * b.l[i] + t[i + j] + c;
+        t[i + j] = (uint64_t)s;
+        c = s >> 64;
+      }
+      for (int j = i + 4; j < 8; j++) {  // (the sum stays below 2^511: no carry out of t[7])
+        const u128 s = (u128)t[j] + c;
+        t[j] = (uint64_t)s;
+        c = s >> 64;
+      }
+    }
+  }
+  for (int i = 0; i < 4; i++) {
+    const uint64_t m = t[i] * NINV;
+    u128 c = 0;
+    for (int j = 0; j < 4; j++) {
+      const u128 s = (u128)m * MOD[j] + t[i + j] + c;
+      t[i + j] = (uint64_t)s;
+      c = s >> 64;
+    }
+    for (int j = i + 4; j < 8; j++) {
+      const u128 s = (u128)t[j] + c;
+      t[j] = (uint64_t)s;
+      c = s >> 64;
+    }
+  }
+  return add_lazy(E{{t[4], t[5], t[6], t[7]}}, E{{0, 0, 0, 0}});
+}
+
 inline E to_mont(const E& a) { return mul(a, E{{R2[0], R2[1], R2[2], R2[3]}}); }
 inline E from_mont(const E& a) { return mul(a, E{{1, 0, 0, 0}}); }
 
@@ -189,7 +230,7 @@ struct Spec3 {
 inline void apply_mds3(E (&s)[3], const E* m) {
   E o[3];
   for (int i = 0; i < 3; i++)
-    o[i] = add_lazy(add_lazy(mul_lazy(s[0], m[3 * i]), mul_lazy(s[1], m[3 * i + 1])), mul_lazy(s[2], m[3 * i + 2]));
+    o[i] = mul_sum3_lazy(s[0], m[3 * i], s[1], m[3 * i + 1], s[2], m[3 * i + 2]);
   for (int i = 0; i < 3; i++) s[i] = o[i];
 }
 
@@ -207,7 +248,7 @@ inline void permute3(E (&s)[3]) {
   for (int r = 0; r < Spec3::RP; r++) {
     s[0] = add_lazy(pow5(s[0]), sp.partial[r]);
     const E* row = sp.sparse.data() + r * 5;  // row (3) || col_hat (2)
-    const E s0 = add_lazy(add_lazy(mul_lazy(s[0], row[0]), mul_lazy(s[1], row[1])), mul_lazy(s[2], row[2]));
+    const E s0 = mul_sum3_lazy(s[0], row[0], s[1], row[1], s[2], row[2]);
     for (int i = 1; i < 3; i++) s[i] = add_lazy(s[i], mul_lazy(s[0], row[3 + i - 1]));
     s[0] = s0;
   }

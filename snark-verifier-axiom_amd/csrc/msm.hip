@@ -501,11 +501,13 @@ __global__ void __launch_bounds__(kBlock) k_bin_scan_chunks(uint32_t* __restrict
 // Block-major counts (bcnt[blk * nk + key]): one 1024-thread block per 32 keys.  Thread (grp, kk)
 // walks rows grp * per .. of key 32 tile + kk, so each row access of a wave reads or writes two whole
 // 128-B lines; exclusive scan over blocks in place, total -> btot.
+template <int KT>  // keys per tile (32 or 16): 1024 / KT row groups per block
 __global__ void __launch_bounds__(1024) k_bin_scan_tiles(uint32_t* __restrict__ bcnt, uint32_t nblk, uint32_t nk,
                                                          uint32_t* __restrict__ btot) {
-  __shared__ uint32_t part[32][33];
-  const uint32_t kk = threadIdx.x & 31, grp = threadIdx.x >> 5, key = blockIdx.x * 32 + kk;
-  const uint32_t per = (nblk + 31) / 32, lo = min(nblk, grp * per), hi = min(nblk, lo + per);
+  constexpr int G = 1024 / KT;
+  __shared__ uint32_t part[G][KT + 1];
+  const uint32_t kk = threadIdx.x % KT, grp = threadIdx.x / KT, key = blockIdx.x * KT + kk;
+  const uint32_t per = (nblk + G - 1) / G, lo = min(nblk, grp * per), hi = min(nblk, lo + per);
   const bool live = key < nk;
   uint32_t* c = bcnt + key;
   uint32_t sum = 0;
@@ -515,14 +517,14 @@ __global__ void __launch_bounds__(1024) k_bin_scan_tiles(uint32_t* __restrict__ 
   }
   part[grp][kk] = sum;
   __syncthreads();
-  if (threadIdx.x < 32) {  // per key: exclusive scan over the 32 row groups
+  if (threadIdx.x < KT) {  // per key: exclusive scan over the G row groups
     uint32_t run = 0;
-    for (int g = 0; g < 32; g++) {
+    for (int g = 0; g < G; g++) {
       const uint32_t v = part[g][threadIdx.x];
       part[g][threadIdx.x] = run;
       run += v;
     }
-    if (blockIdx.x * 32 + threadIdx.x < nk) btot[blockIdx.x * 32 + threadIdx.x] = run;
+    if (blockIdx.x * KT + threadIdx.x < nk) btot[blockIdx.x * KT + threadIdx.x] = run;
   }
   __syncthreads();
   if (live) {
@@ -1667,10 +1669,16 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
               phix, p.r29 ? kPhiVtab : p.phi64, check_bases, xcd, bm, w0, nw);
   SV_HIP(hipGetLastError());
   if (ev_sort_mid) SV_HIP(hipEventRecord(ev_sort_mid, st));
-  if (bm)
-    hipLaunchKernelGGL(k_bin_scan_tiles, dim3(cdiv(nwb, 32)), dim3(1024), 0, st, w.bcnt, nblk, nwb, w.btot);
-  else
+  if (bm) {
+    // SVGPU_SCAN_KEYS=16: tiles of 16 keys (twice the blocks, 64 row groups per key); default 32
+    const char* ke = getenv("SVGPU_SCAN_KEYS");
+    if (ke && atoi(ke) == 16)
+      hipLaunchKernelGGL(k_bin_scan_tiles<16>, dim3(cdiv(nwb, 16)), dim3(1024), 0, st, w.bcnt, nblk, nwb, w.btot);
+    else
+      hipLaunchKernelGGL(k_bin_scan_tiles<32>, dim3(cdiv(nwb, 32)), dim3(1024), 0, st, w.bcnt, nblk, nwb, w.btot);
+  } else {
     hipLaunchKernelGGL(k_bin_scan_chunks, dim3(nwb), dim3(kBlock), 0, st, w.bcnt, nblk, w.btot);
+  }
   // (fusing this scan into k_bin_scan_chunks' last block -- device-scope fence + counter -- was
   // measured 12 -> 122 us for that kernel: the fence writes back the XCD's L2)
   hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, w.btot, nwb, w.bstart, so.gst + (size_t)nw * p.B);

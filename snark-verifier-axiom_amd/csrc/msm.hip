@@ -2053,7 +2053,9 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
       // the host pool) becomes the call's SV_ERR_DEVICE instead of std::terminate
       try {
         int st0;
-        while ((st0 = staged.load(std::memory_order_acquire)) == 0) std::this_thread::yield();
+        // also leave when the caller stops before staging piece 0 (its copy failed or threw)
+        while ((st0 = staged.load(std::memory_order_acquire)) == 0 && !stop.load(std::memory_order_relaxed))
+          std::this_thread::yield();
         for (int k = 0; st0 > 0 && k < pieces && !stop.load(std::memory_order_relaxed); k++) {
           const size_t lo = pb[k], hi = pb[k + 1];
           if (k > 0) {
@@ -2087,6 +2089,8 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
       }
     } join{ws, stop};
     {
+      // an exception leaving stage_scalars (host-pool allocation) unwinds through join, whose stop
+      // releases the helper's wait above; SV_GUARD then turns it into the call's error code
       const int rc0 = feed->stage_scalars(pb[0], pb[1], const_cast<Fr*>(scalars) + pb[0], cs, ev[8]);
       if (rc0 != SV_OK) {
         feed_rc = rc0;

@@ -19,6 +19,7 @@
 from __future__ import annotations
 
 import ctypes
+import numbers
 from dataclasses import dataclass
 from typing import Optional, Sequence, Tuple
 
@@ -96,12 +97,13 @@ class KzgAs:
         """KzgAs::create_proof with the default proving key (no blind), accumulation.rs:146-195.
 
         ``transcript``: None or a fresh ``PoseidonTranscript`` -> r from the library's transcript
-        (one call); a used ``PoseidonTranscript`` -> absorbed / squeezed through it; an int -> r."""
+        (one call); a used ``PoseidonTranscript`` -> absorbed / squeezed through it; an integer
+        (``numbers.Integral``: int, numpy integers) -> r."""
         if len(instances) == 0:
             raise ReferencePanic("assertion failed: !instances.is_empty()")
         from .poseidon import PoseidonTranscript
-        if isinstance(transcript, int):
-            return KzgAs._accumulate(instances, transcript)
+        if isinstance(transcript, numbers.Integral):  # int, numpy integers, ...: r itself
+            return KzgAs._accumulate(instances, int(transcript))
         if transcript is not None and (not isinstance(transcript, PoseidonTranscript) or transcript.buf.buf
                                        or transcript.buf.t != 3):
             # a transcript with pending input (or another kind): absorb and squeeze through it

@@ -9,13 +9,19 @@
 //!
 //! Every safe wrapper returns `None` on a device error (no GPU, HIP error) so the caller keeps
 //! the reference's own CPU path; reference panics (empty input) are reproduced as panics.
+//!
+//! Toolchain: the crate builds with the reference's pinned `nightly-2022-10-28`
+//! (`rust-toolchain`), so it uses only std items stable at that date and enables no nightly
+//! feature: process-wide lazy values are `std::sync::Once` + atomics, not `OnceLock` (stable
+//! only from 1.70).  tests/test_rust_shim.py keeps a denylist of later std items.
 #![allow(clippy::missing_safety_doc)]
 
 use halo2curves::bn256::{Fq, Fr, G1Affine, G2Affine};
 use halo2curves::pairing::Engine;
 use halo2curves::CurveAffine;
 use std::os::raw::{c_char, c_int, c_void};
-use std::sync::OnceLock;
+use std::sync::atomic::{AtomicBool, AtomicUsize, Ordering};
+use std::sync::Once;
 
 pub const SV_CANONICAL: c_int = 0;
 pub const SV_MONTGOMERY: c_int = 1;
@@ -175,25 +181,34 @@ pub fn last_error() -> String {
 
 /// Smallest MSM routed to the GPU (SVGPU_MIN_MSM, default 64): below it the launch dominates.
 pub fn min_msm() -> usize {
-    static MIN: OnceLock<usize> = OnceLock::new();
-    *MIN.get_or_init(|| std::env::var("SVGPU_MIN_MSM").ok().and_then(|v| v.parse().ok()).unwrap_or(64))
+    static INIT: Once = Once::new();
+    static MIN: AtomicUsize = AtomicUsize::new(64);
+    // call_once's completion happens-before every later return from it, so a relaxed load sees it
+    INIT.call_once(|| {
+        if let Some(v) = std::env::var("SVGPU_MIN_MSM").ok().and_then(|v| v.parse::<usize>().ok()) {
+            MIN.store(v, Ordering::Relaxed);
+        }
+    });
+    MIN.load(Ordering::Relaxed)
 }
 
 /// True when a GPU is usable, SVGPU_DISABLE is unset and halo2curves' memory layout is the one
 /// the zero-copy calls assume (checked once, process-wide).
 pub fn available() -> bool {
-    static READY: OnceLock<bool> = OnceLock::new();
-    *READY.get_or_init(|| {
+    static INIT: Once = Once::new();
+    static READY: AtomicBool = AtomicBool::new(false);
+    INIT.call_once(|| {
         if std::env::var_os("SVGPU_DISABLE").is_some() {
-            return false;
+            return;
         }
         let layout_ok = std::mem::size_of::<G1Affine>() == 64
             && std::mem::size_of::<G2Affine>() == 128
             && std::mem::size_of::<Fr>() == 32
             && unsafe { std::mem::transmute::<Fq, [u64; 4]>(Fq::one()) }
                 == [0xd35d438dc58f0d9d, 0x0a78eb28f5c70b3d, 0x666ea36f7879462c, 0x0e0a77c19a07df2f];
-        layout_ok && unsafe { sv_init(0) } == SV_OK
-    })
+        READY.store(layout_ok && unsafe { sv_init(0) } == SV_OK, Ordering::Relaxed);
+    });
+    READY.load(Ordering::Relaxed)
 }
 
 /// Reinterpret a generic curve's slices as BN254 ones.  Both element types are checked at run
@@ -343,8 +358,11 @@ pub fn accumulate(lhs: &[G1Affine], rhs: &[G1Affine], r: &Fr) -> Option<(G1Affin
 /// KzgAs::create_proof without blind, challenge included (pcs/kzg/accumulation.rs:146-195): the
 /// accumulators are absorbed into a Poseidon transcript (fresh when `sponge_state` is None, else
 /// continuing from that state, which receives the state after the squeeze) and r is squeezed
-/// (:158-176); returns (Σ rⁱ lhsᵢ, Σ rⁱ rhsᵢ, r).  `Err(true)` = an identity accumulator point
-/// (the reference's Error::Transcript), `Err(false)` = device error.
+/// (:158-176); returns (Σ rⁱ lhsᵢ, Σ rⁱ rhsᵢ, r).  `Err(true)` = an identity accumulator point,
+/// which the reference reports as `Error::Transcript` ("Invalid elliptic curve point encoding in
+/// proof", transcript/halo2.rs:214-226).  `Err(false)` = anything else the library refused: a
+/// device error, or an argument error that is not the identity case (an unreduced coordinate or
+/// sponge-state element); the caller then keeps its own CPU path, which reports such input itself.
 pub fn create_proof(lhs: &[G1Affine], rhs: &[G1Affine], sponge_state: Option<&mut [Fr; 3]>)
                     -> Result<(G1Affine, G1Affine, Fr), bool> {
     assert!(!lhs.is_empty());
@@ -358,10 +376,14 @@ pub fn create_proof(lhs: &[G1Affine], rhs: &[G1Affine], sponge_state: Option<&mu
     };
     match rc {
         SV_OK => Ok((g1_out(ol), g1_out(or), r)),
-        SV_ERR_ARG => Err(true),
+        SV_ERR_ARG if last_error().starts_with(IDENTITY_MSG) => Err(true),
         _ => Err(false),
     }
 }
+
+/// Prefix of `sv_last_error()` for an identity accumulator point (csrc/api.cpp), the reference's
+/// Error::Transcript message.
+pub const IDENTITY_MSG: &str = "Invalid elliptic curve point encoding in proof";
 
 /// Many small MSMs in one launch: MSM k = terms offsets[k]..offsets[k+1].
 pub fn msm_batch(scalars: &[Fr], bases: &[G1Affine], offsets: &[u64]) -> Option<Vec<G1Affine>> {

@@ -79,6 +79,9 @@ def test_accumulate_golden_and_decide(gpu, golden_decider):
     accs = [svgpu.KzgAccumulator(pt(l), pt(r)) for l, r in zip(a["lhs"], a["rhs"])]
     out = svgpu.KzgAs.create_proof(accs, int(a["r"], 16))
     assert [out.lhs, out.rhs] == [pt(a["expected"][0]), pt(a["expected"][1])]
+    # an int-like r (numbers.Integral, e.g. a numpy integer) is r too, not a transcript
+    small = svgpu.KzgAs.create_proof(accs, np.uint64(12345))
+    assert (small.lhs, small.rhs) == b.accumulate([(pt(l), pt(r)) for l, r in zip(a["lhs"], a["rhs"])], 12345)
 
 
 def test_aggregation_64_end_to_end(gpu):

@@ -123,3 +123,60 @@ def test_generic_helpers_check_types_before_casting():
     body = _fn_body(rs, "is_bn256")
     assert "M::G1Affine" in body and "M::G2Affine" in body
     assert re.search(r"pub fn is_bn256<M: Engine>\(\)", rs)
+
+
+# std items (and syntax) stabilised after the reference's pinned toolchain, nightly-2022-10-28
+# (/root/reference/rust-toolchain:1; Rust 1.66/1.67-nightly), each with its stable release.  A crate
+# that uses one does not build where the reference builds unless its crate root enables the
+# matching nightly feature, which this crate does not do.
+_AFTER_TOOLCHAIN = {
+    r"\bOnceLock\b": "1.70",
+    r"\bOnceCell\b": "1.70 (std::cell)",
+    r"\bLazyLock\b": "1.80",
+    r"\bLazyCell\b": "1.80",
+    r"\.is_some_and\(": "1.70",
+    r"\.is_ok_and\(": "1.70",
+    r"\.is_none_or\(": "1.82",
+    r"\.inspect_err\(": "1.76",
+    r"\.div_ceil\(": "1.73",
+    r"\.ilog2\(|\.ilog10\(|checked_ilog": "1.67",
+    r"\bIsTerminal\b": "1.70",
+    r"from_bytes_until_nul": "1.69",
+    r"\.first_chunk\(|\.split_first_chunk\(": "1.77",
+    r"\bis_sorted\(": "1.82",
+    r"\bbool::then_some\b": "1.62 (allowed)",
+}
+
+
+def _code_without_comments(rs):
+    return "\n".join(line.split("//", 1)[0] for line in rs.splitlines())
+
+
+def test_crate_uses_only_std_items_of_the_reference_toolchain():
+    """The drop-in must compile where the reference compiles (OnceLock broke that)."""
+    toolchain = "/root/reference/rust-toolchain"
+    if os.path.exists(toolchain):
+        assert open(toolchain).read().strip() == "nightly-2022-10-28"
+    rs = open(os.path.join(ROOT, "snark-verifier-gpu", "src", "lib.rs")).read()
+    code = _code_without_comments(rs)
+    features = re.findall(r"#!\[feature\(([^)]*)\)\]", code)
+    hits = []
+    for pat, since in _AFTER_TOOLCHAIN.items():
+        if "allowed" in since:
+            continue
+        if re.search(pat, code):
+            hits.append(f"{pat} (stable {since})")
+    assert not hits, f"lib.rs uses std items newer than nightly-2022-10-28: {hits}; features: {features}"
+    # the lazy values use Once + atomics (stable since 1.0 / 1.24)
+    assert "static INIT: Once = Once::new();" in code
+
+
+def test_create_proof_maps_only_the_identity_case_to_the_transcript_error():
+    """SV_ERR_ARG also covers unreduced coordinates; only the identity message is the
+    reference's Error::Transcript."""
+    rs = open(os.path.join(ROOT, "snark-verifier-gpu", "src", "lib.rs")).read()
+    body = _fn_body(rs, "create_proof")
+    assert "SV_ERR_ARG if last_error().starts_with(IDENTITY_MSG) => Err(true)" in body
+    api = open(os.path.join(ROOT, "snark-verifier-axiom_amd", "csrc", "api.cpp")).read()
+    msg = re.search(r'pub const IDENTITY_MSG: &str = "([^"]+)";', rs).group(1)
+    assert f'sv::set_error("{msg} (accumulator' in api

@@ -1,0 +1,103 @@
+// Microbenchmark (round 5): does v_mad_u64_u32 leave issue slots for other VALU instructions on
+// gfx950?  Each kernel runs 8 independent v_mad_u64_u32 accumulator chains per iteration and, in
+// the mixed variants, N other VALU instructions per mad on their own registers (no dependence on
+// the mads).  If a mixed variant takes the time of the pure one, those instructions co-issue beside
+// the mads; if it takes the sum, every VALU instruction costs issue time.
+// Occupancy: blocks of 256 threads, launch bounds (256, 4) -> 4 waves per SIMD, as k_accumulate.
+// Usage: ./ubench_issue
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e = (x);                                                        \
+    if (e != hipSuccess) {                                                     \
+      printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__);          \
+      return 1;                                                                \
+    }                                                                          \
+  } while (0)
+
+// OP: 0 none, 1 v_add_u32, 2 v_and_b32, 3 v_lshrrev_b64, 4 v_mul_lo_u32, 5 v_lshl_add_u64,
+//     6 v_add_co/v_addc pair (counted as 2), 7 v_bfe_u32
+template <int OP, int N>
+__global__ void __launch_bounds__(256, 4) k_mix(uint64_t* out, int iters) {
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t acc[8], w[8];
+  uint32_t a[8], b[8], x[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    acc[j] = tid + j;
+    a[j] = tid * 3 + j;
+    b[j] = tid ^ (j * 77);
+    x[j] = tid * 7 + j;
+    w[j] = (uint64_t)tid << 20 | j;
+  }
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      asm volatile("v_mad_u64_u32 %0, s[0:1], %1, %2, %0" : "+v"(acc[j]) : "v"(a[j]), "v"(b[j]) : "s0", "s1");
+#pragma unroll
+      for (int r = 0; r < N; r++) {
+        const int k = (j + r) & 7;
+        if constexpr (OP == 1) asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[k]) : "v"(a[k]));
+        if constexpr (OP == 2) asm volatile("v_and_b32 %0, %0, %1" : "+v"(x[k]) : "v"(b[k]));
+        if constexpr (OP == 3) asm volatile("v_lshrrev_b64 %0, 3, %0" : "+v"(w[k]));
+        if constexpr (OP == 4) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x[k]) : "v"(b[k]));
+        if constexpr (OP == 5) asm volatile("v_lshl_add_u64 %0, %0, 1, %1" : "+v"(w[k]) : "v"(w[(k + 1) & 7]));
+        if constexpr (OP == 6)
+          asm volatile("v_add_co_u32 %0, vcc, %0, %1\n\tv_addc_co_u32 %2, vcc, 0, %2, vcc"
+                       : "+v"(x[k]), "+v"(a[(k + 3) & 7]) : "v"(b[k]) : "vcc");
+        if constexpr (OP == 7) asm volatile("v_bfe_u32 %0, %0, 3, 29" : "+v"(x[k]));
+      }
+    }
+  }
+  uint64_t s = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) s += acc[j] + x[j] + w[j] + a[j];
+  out[tid] = s;
+}
+
+template <typename K>
+static float run(const char* name, K kern, uint64_t* d, double others_per_mad, float base) {
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  const int blocks = 8192, bs = 256, iters = 1000;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(bs), 0, 0, d, 10);
+  if (hipDeviceSynchronize() != hipSuccess) return -1.f;
+  float best = 1e30f;
+  for (int rep = 0; rep < 3; rep++) {
+    hipEventRecord(e0);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(bs), 0, 0, d, iters);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (ms < best) best = ms;
+  }
+  const double waves = (double)blocks * bs / 64, mads = waves * iters * 8;
+  // SIMD-cycles per wave-instruction at 2.4 GHz over 1024 SIMDs
+  const double simd_cycles = best * 1e-3 * 2.4e9 * 1024;
+  printf("%-22s %8.3f ms  mad lane-op/clk/CU %6.1f  cycles per mad %5.2f  extra vs pure %+6.2f cycles per other op\n",
+         name, best, mads * 64 / (best * 1e-3) / 2.4e9 / 256, simd_cycles / mads,
+         others_per_mad > 0 ? (best - base) * 1e-3 * 2.4e9 * 1024 / (mads * others_per_mad) : 0.0);
+  return best;
+}
+
+int main() {
+  void* d;
+  CK(hipMalloc(&d, 64 << 20));
+  const float base = run("mad only", k_mix<0, 0>, (uint64_t*)d, 0, 0);
+  run("mad + 1 add_u32", k_mix<1, 1>, (uint64_t*)d, 1, base);
+  run("mad + 2 add_u32", k_mix<1, 2>, (uint64_t*)d, 2, base);
+  run("mad + 4 add_u32", k_mix<1, 4>, (uint64_t*)d, 4, base);
+  run("mad + 1 and_b32", k_mix<2, 1>, (uint64_t*)d, 1, base);
+  run("mad + 1 lshrrev_b64", k_mix<3, 1>, (uint64_t*)d, 1, base);
+  run("mad + 1 mul_lo_u32", k_mix<4, 1>, (uint64_t*)d, 1, base);
+  run("mad + 1 lshl_add_u64", k_mix<5, 1>, (uint64_t*)d, 1, base);
+  run("mad + 1 add_co/addc", k_mix<6, 1>, (uint64_t*)d, 2, base);
+  run("mad + 1 bfe_u32", k_mix<7, 1>, (uint64_t*)d, 1, base);
+  run("mad + 8 add_u32", k_mix<1, 8>, (uint64_t*)d, 8, base);
+  return 0;
+}

@@ -119,6 +119,10 @@ struct Staging {
     if (bytes) SV_HIP(hipMemcpyAsync(d[i], h, bytes, hipMemcpyHostToDevice, lease.get()->stream));
     return SV_OK;
   }
+  int put_at(int i, size_t offset, const void* h, size_t bytes) {
+    if (bytes) SV_HIP(hipMemcpyAsync(d[i] + offset, h, bytes, hipMemcpyHostToDevice, lease.get()->stream));
+    return SV_OK;
+  }
   int get(void* h, int i, size_t bytes) {
     if (bytes) SV_HIP(hipMemcpyAsync(h, d[i], bytes, hipMemcpyDeviceToHost, lease.get()->stream));
     return SV_OK;
@@ -128,6 +132,14 @@ struct Staging {
     return SV_OK;
   }
 };
+
+// Small MSMs (at most kSmallMsmTerms terms each, msm.hpp) go through msm_batch_windows_host: window
+// sums on the device, the window Horner on the host.  SVGPU_SMALL_MSM=0 keeps the single-MSM
+// pipeline (read per call; results identical).
+bool small_msm_off() {
+  const char* e = getenv("SVGPU_SMALL_MSM");
+  return e && atoi(e) == 0;
+}
 
 // pieces of a host-fed MSM (SVGPU_H2D_PIECES; unset = 0: the MSM plan picks, see msm_run_impl):
 // piece k + 1's transfer overlaps piece k's sort and accumulation
@@ -439,15 +451,37 @@ int sv_bn254_kzg_accumulate(const sv_g1_affine* lhs, const sv_g1_affine* rhs, si
   }
   if (resolve_gpus(1) == 0) return SV_ERR_DEVICE;
   int dev = runtime_device_id(0);
+  if (n <= kSmallMsmTerms && !small_msm_off()) {
+    // Round 5: the two MSMs as ONE small batch (msm_batch_windows_host): r^i on the host (n Fr
+    // products, ~1 us; k_powers was a 28 us serial chain on one lane plus a synchronisation), the
+    // window sums of both MSMs in one launch, the window Horner of both on the host.
+    namespace fr = sv::host::fr;
+    fr::E rm;
+    memcpy(rm.l, r->l, 32);
+    if (form != SV_MONTGOMERY) rm = fr::to_mont(rm);
+    std::vector<sv_fe> pw(2 * n);
+    fr::E acc = fr::one();
+    for (size_t i = 0; i < n; i++) {
+      memcpy(pw[i].l, acc.l, 32);
+      pw[n + i] = pw[i];
+      acc = fr::mul(acc, rm);
+    }
+    const uint64_t off[3] = {0, n, 2 * n};
+    Staging sg(dev);
+    SV_TRY(sg.init({2 * n * sizeof(sv_g1_affine), 2 * n * sizeof(sv_fe), sizeof off}));
+    SV_TRY(sg.put(0, lhs, n * sizeof(sv_g1_affine)));
+    SV_TRY(sg.put_at(0, n * sizeof(sv_g1_affine), rhs, n * sizeof(sv_g1_affine)));
+    SV_TRY(sg.put(1, pw.data(), 2 * n * sizeof(sv_fe)));
+    SV_TRY(sg.put(2, off, sizeof off));
+    Xyzz ab[2];
+    SV_TRY(msm_batch_windows_host(sg.at(0), sg.at(1), sg.at<const uint64_t>(2), 2, n, SV_MONTGOMERY, form, dev,
+                                  sg.lease.get()->stream, ab));
+    affine_out(ab[0], form, out_lhs);
+    affine_out(ab[1], form, out_rhs);
+    return SV_OK;
+  }
   Staging sg(dev);
-  SV_TRY(sg.init({n * sizeof(sv_g1_affine), n * sizeof(sv_g1_affine), n * sizeof(sv_fe), sizeof(sv_fe)}));
-  SV_TRY(sg.put(0, lhs, n * sizeof(sv_g1_affine)));
-  SV_TRY(sg.put(1, rhs, n * sizeof(sv_g1_affine)));
-  SV_TRY(sg.put(3, r, sizeof(sv_fe)));
-  SV_TRY(sg.sync());
-  SV_TRY(powers_device(sg.at(3), form, n, form, sg.at(2), sg.lease.get()->stream));
-  SV_TRY(sg.sync());
-  // the lhs and rhs MSMs share the scalars and are independent: run them concurrently (each call
+  SV_TRY(sg.init({n * sizeof(sv_g1_affine), n * sizeof(sv_g1_affine), n * sizeof(sv_fe), sizeof(sv_fe)}));  // the lhs and rhs MSMs share the scalars and are independent: run them concurrently (each call
   // leases its own stream + workspace), one on the caller and one on a pool worker
   Xyzz ab[2];
   int rc2[2] = {SV_OK, SV_OK};

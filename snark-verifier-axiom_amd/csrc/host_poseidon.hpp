@@ -5,7 +5,7 @@
 // fresh PoseidonTranscript (snark-verifier-sdk/src/halo2/aggregation.rs:235-242) and squeezes r:
 // 2n field elements -> n + 1 dependent t = 3 permutations, a serial chain of ~260 dependent Fr
 // products each.  A GPU lane runs a dependent Fr product in ~0.6 us (one wave), so one
-// sponge on the device takes ~20 ms at n = 64; here it takes ~4 us per permutation.  The batched
+// sponge on the device takes ~20 ms at n = 64; here it takes ~6.4 us per permutation.  The batched
 // many-sponge form (one lane per transcript) stays on the device (poseidon.hip).
 //
 // The schedule is the reference's optimised one (OptimizedPoseidonSpec, poseidon.rs:230-313;
@@ -13,6 +13,7 @@
 // oracle/poseidon.py, pinned by the reference KATs poseidon/tests.rs:34-85): folded round
 // constants, a pre-sparse MDS after the first full half, sparse partial-round matrices.
 #pragma once
+#include <cstddef>
 #include <cstdint>
 #include <vector>
 
@@ -139,31 +140,41 @@ inline E add_lazy(const E& a, const E& b) {
   return r;
 }
 
-// a0 b0 + a1 b1 + a2 b2 with ONE Montgomery reduction (an MDS row over constants): a_i below 2r,
-// b_i below r.  The 512-bit sum is below 6 r^2, so the reduced value is below 6 r (r / 2^256) + r
-// < 2.14 r, wrapped below 2r like add_lazy.  Two reductions fewer than three mul_lazy.
-inline E mul_sum3_lazy(const E& a0, const E& b0, const E& a1, const E& b1, const E& a2, const E& b2) {
-  uint64_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const E* as[3] = {&a0, &a1, &a2};
-  const E* bs[3] = {&b0, &b1, &b2};
-  for (int k = 0; k < 3; k++) {
-    const E& a = *as[k];
-    const E& b = *bs[k];
-    for (int i = 0; i < 4; i++) {
-      u128 c = 0;
-      for (int j = 0; j < 4; j++) {
-        const u128 s = (u128)a.l[j] * b.l[i] + t[i + j] + c;
-        t[i + j] = (uint64_t)s;
-        c = s >> 64;
-      }
-      for (int j = i + 4; j < 8; j++) {  // (the sum stays below 2^511: no carry out of t[7])
-        const u128 s = (u128)t[j] + c;
-        t[j] = (uint64_t)s;
-        c = s >> 64;
-      }
-    }
-  }
+// ---- Wide products (round 5): 512-bit unreduced products summed before ONE reduction, so the
+// partial rounds' critical path is sqr -> sqr -> (one product + reduction) per round (below).
+struct W {  // 512-bit
+  uint64_t l[8];
+};
+inline W mul_wide(const E& a, const E& b) {  // a b, operand scanning (as mul_lazy's rows)
+  W r;
+  for (int i = 0; i < 8; i++) r.l[i] = 0;
   for (int i = 0; i < 4; i++) {
+    u128 c = 0;
+    for (int j = 0; j < 4; j++) {
+      const u128 s = (u128)a.l[j] * b.l[i] + r.l[i + j] + c;
+      r.l[i + j] = (uint64_t)s;
+      c = s >> 64;
+    }
+    r.l[i + 4] = (uint64_t)c;
+  }
+  return r;
+}
+inline W add_wide(const W& a, const W& b) {
+  W r;
+  u128 c = 0;
+  for (int i = 0; i < 8; i++) {
+    const u128 s = (u128)a.l[i] + b.l[i] + c;
+    r.l[i] = (uint64_t)s;
+    c = s >> 64;
+  }
+  return r;
+}
+// T / 2^256 mod r for T < 2^256 r + ... : (T + m r) / 2^256 < T / 2^256 + r; wrapped below 2r
+// (one conditional subtraction of 2r) when that is below 4r, i.e. for T < 3 * 2^256 r
+inline E redc_wide(const W& T) {
+  uint64_t t[8];
+  for (int i = 0; i < 8; i++) t[i] = T.l[i];
+  for (int i = 0; i < 4; i++) {  // T + m r < 2^512 for the bounds above: no carry out of t[7]
     const uint64_t m = t[i] * NINV;
     u128 c = 0;
     for (int j = 0; j < 4; j++) {
@@ -179,6 +190,7 @@ inline E mul_sum3_lazy(const E& a0, const E& b0, const E& a1, const E& b1, const
   }
   return add_lazy(E{{t[4], t[5], t[6], t[7]}}, E{{0, 0, 0, 0}});
 }
+inline E sqr_lazy(const E& a) { return mul_lazy(a, a); }
 
 inline E to_mont(const E& a) { return mul(a, E{{R2[0], R2[1], R2[2], R2[3]}}); }
 inline E from_mont(const E& a) { return mul(a, E{{1, 0, 0, 0}}); }
@@ -193,11 +205,6 @@ inline bool is_reduced(const E& a) {
     if (a.l[i] > MOD[i]) return false;
   }
   return false;
-}
-
-inline E pow5(const E& x) {  // x < 2r -> result < 2r
-  const E x2 = mul_lazy(x, x);
-  return mul_lazy(mul_lazy(x2, x2), x);
 }
 
 // the t = 3 constants of poseidon_consts.hpp (8 x u32 Montgomery limbs each) as 4 x u64
@@ -227,35 +234,42 @@ struct Spec3 {
   }
 };
 
-inline void apply_mds3(E (&s)[3], const E* m) {
-  E o[3];
+// One full round in the plain order: s_j <- s_j^5 + c_j (c = nullptr: none), then each MDS row as
+// ONE reduction of three wide products (below 3 (2r) r = 6 r^2 < 3 * 2^256 r).
+inline void full_round3p(E (&s)[3], const E* m, const E* c) {
+  E x[3];
+  for (int j = 0; j < 3; j++) {
+    const E x2 = sqr_lazy(s[j]);
+    x[j] = mul_lazy(sqr_lazy(x2), s[j]);
+    if (c) x[j] = add_lazy(x[j], c[j]);
+  }
   for (int i = 0; i < 3; i++)
-    o[i] = mul_sum3_lazy(s[0], m[3 * i], s[1], m[3 * i + 1], s[2], m[3 * i + 2]);
-  for (int i = 0; i < 3; i++) s[i] = o[i];
+    s[i] = redc_wide(add_wide(mul_wide(x[0], m[3 * i]), add_wide(mul_wide(x[1], m[3 * i + 1]), mul_wide(x[2], m[3 * i + 2]))));
 }
 
 // Poseidon::permutation (poseidon.rs:469-500) after the inputs were added: the bare HADES map in
 // the optimised schedule, as the device's sv::permute<3> runs it (Montgomery form).  Every word
 // stays below 2r inside (lazy products and sums); the state is canonical again at the end.
+// Round 5: a partial round forms row1 s1 + row2 s2 (two wide products) beside the pow5 chain and
+// reduces the row once with (s0^5 + c) row0 added: the same products as before, the chain shorter
+// by the row's other two products (6.72 -> 6.40 us per permutation on the box's EPYC 9575F,
+// tools/ubench_host_poseidon.cpp; folding the constants to shorten it further did more work and
+// measured 7.6 us: the host chain is bound by multiplier throughput as much as by latency).
 inline void permute3(E (&s)[3]) {
   const Spec3& sp = Spec3::get();
   constexpr int H = Spec3::RF / 2;
   for (int i = 0; i < 3; i++) s[i] = add_lazy(s[i], sp.start[i]);  // absorb_with_pre_constants
-  for (int r = 1; r <= H; r++) {
-    for (int i = 0; i < 3; i++) s[i] = add_lazy(pow5(s[i]), sp.start[r * 3 + i]);
-    apply_mds3(s, r < H ? sp.mds.data() : sp.pre.data());
-  }
+  for (int r = 1; r <= H; r++) full_round3p(s, r < H ? sp.mds.data() : sp.pre.data(), &sp.start[r * 3]);
   for (int r = 0; r < Spec3::RP; r++) {
-    s[0] = add_lazy(pow5(s[0]), sp.partial[r]);
     const E* row = sp.sparse.data() + r * 5;  // row (3) || col_hat (2)
-    const E s0 = mul_sum3_lazy(s[0], row[0], s[1], row[1], s[2], row[2]);
-    for (int i = 1; i < 3; i++) s[i] = add_lazy(s[i], mul_lazy(s[0], row[3 + i - 1]));
-    s[0] = s0;
+    const E x = s[0];
+    const W u = add_wide(mul_wide(s[1], row[1]), mul_wide(s[2], row[2]));  // beside the pow5 chain
+    const E x2 = sqr_lazy(x);
+    const E x5c = add_lazy(mul_lazy(sqr_lazy(x2), x), sp.partial[r]);
+    s[0] = redc_wide(add_wide(u, mul_wide(x5c, row[0])));
+    for (int i = 1; i < 3; i++) s[i] = add_lazy(s[i], mul_lazy(x5c, row[3 + i - 1]));
   }
-  for (int r = 0; r < H; r++) {
-    for (int i = 0; i < 3; i++) s[i] = r < H - 1 ? add_lazy(pow5(s[i]), sp.end[r * 3 + i]) : pow5(s[i]);
-    apply_mds3(s, sp.mds.data());
-  }
+  for (int r = 0; r < H; r++) full_round3p(s, sp.mds.data(), r < H - 1 ? &sp.end[r * 3] : nullptr);
   for (int i = 0; i < 3; i++) s[i] = reduce_once(s[i].l, 0);  // [0, 2r) -> canonical
 }
 

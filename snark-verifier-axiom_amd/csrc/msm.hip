@@ -47,6 +47,7 @@
 #include "glv.hpp"
 #include "host_ec.hpp"
 #include "msm.hpp"
+#include "msm_batch.hpp"
 #include "quad.hpp"
 #include "runtime.hpp"
 
@@ -1826,6 +1827,21 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   if (!lease.ok()) return SV_ERR_DEVICE;
   Workspace* ws = lease.get();
   hipStream_t st = ws->stream;
+  // Small MSMs (round 5): the window sums on the device, the window Horner on the host
+  // (msm_batch_windows_host, msm_batch.hip): the pipeline below is latency-bound there (a 64-term
+  // MSM took ~0.35 ms: a dozen launches, serial accumulate chunks, the reduction kernels and a host
+  // Horner over 52 windows).  SVGPU_SMALL_MSM=0 keeps the pipeline (read per call).
+  if (n <= kSmallMsmTerms && !(getenv("SVGPU_SMALL_MSM") && atoi(getenv("SVGPU_SMALL_MSM")) == 0)) {
+    g_last_stats = sv_msm_stats{};
+    if (!feed) return msm_batch_windows_host(d_bases, d_scalars, nullptr, 1, n, form, form, device, st, out);
+    const size_t sbytes = Workspace::aligned(n * sizeof(Fr));
+    SV_TRY(ws->reserve_in(sbytes + n * sizeof(G1Aff)));
+    void* ds = ws->inbuf;
+    void* db = ws->inbuf + sbytes;
+    SV_TRY(feed->stage_scalars(0, n, ds, st, ws->ev[0]));
+    SV_TRY(feed->stage_bases(0, n, db, st, ws->ev[1]));
+    return msm_batch_windows_host(db, ds, nullptr, 1, n, form, form, device, st, out);
+  }
   MsmPlan p = msm_plan(n);
   // host-fed inputs arrive in pieces (piece_bounds): piece k is sorted on the sort stream once its
   // scalars have landed and accumulated on the compute stream once its bases have, while later

@@ -32,6 +32,10 @@ struct MsmPlan {
 
 MsmPlan msm_plan(size_t n);
 
+// MSMs of at most this many terms skip the pipeline: window sums on the device, the window Horner on
+// the host (msm_batch_windows_host); SVGPU_SMALL_MSM=0 keeps the pipeline for them.
+constexpr size_t kSmallMsmTerms = 256;
+
 // Device-resident MSM on `device`; result (XYZZ, Montgomery) on the host.
 int msm_run_device(const void* d_bases, const void* d_scalars, size_t n, int form, int device,
                    hipStream_t stream, host::Xyzz* out);

@@ -26,6 +26,7 @@
 
 #include "curve.hpp"
 #include "glv.hpp"
+#include "host_ec.hpp"
 #include "msm_batch.hpp"
 #include "quad.hpp"
 #include "runtime.hpp"
@@ -1053,6 +1054,81 @@ int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t*
 }
 
 uint64_t msm_batch_fused_redone() { return g_fused_redone.load(std::memory_order_relaxed); }
+
+// ---- Small batches with the window Horner on the host (round 5).  A batch of a few MSMs of at most
+// kQMaxTerms terms -- KzgAs::create_proof's two r^i MSMs (accumulation.rs:177-192), a native
+// verifier's per-proof MSMs -- is bound by its serial tail: the Horner over the 26 windows of a
+// 128-bit GLV half (130 doublings) is ~475 dependent product levels on one GPU wave, ~0.25 ms, but
+// ~20 us on the host (host_ec.hpp).  The device forms every window sum T_w (k_batch_prep +
+// k_batch_windows_q: ~16 quad-operation levels), one copy brings them back, the host combines them.
+// d_offsets = nullptr: one MSM of max_terms terms.
+int msm_batch_windows_host(const void* d_bases, const void* d_scalars, const uint64_t* d_offsets, size_t count,
+                           size_t max_terms, int scalar_form, int base_form, int device, hipStream_t stream,
+                           host::Xyzz* out) {
+  if (count == 0) return SV_OK;
+  if (max_terms == 0 || max_terms > (size_t)kQMaxTerms || count > 0xffffu) {
+    set_error("msm_batch_windows_host: %zu MSMs of up to %zu terms (at most %d terms)", count, max_terms, kQMaxTerms);
+    return SV_ERR_ARG;
+  }
+  WsLease lease(device, stream);
+  if (!lease.ok()) return SV_ERR_DEVICE;
+  Workspace* ws = lease.get();
+  hipStream_t st = ws->stream;
+  const size_t nT = count * kQW;
+  const size_t dig_bytes = count * kQW * 2 * max_terms;
+  const size_t pts_bytes = count * 2 * max_terms * sizeof(G1Aff);
+  const size_t t_off = 256;  // the error word, then the window sums: ONE copy back
+  const size_t back = t_off + nT * sizeof(G1Xyzz);  // bytes copied back
+  SV_TRY(ws->reserve(t_off + Workspace::aligned(nT * sizeof(G1Xyzz)) + Workspace::aligned(dig_bytes) +
+                     Workspace::aligned(pts_bytes) + 256));
+  SV_TRY(ws->reserve_pinned(Workspace::aligned(back) + 16));
+  unsigned char* blk = ws->carve<unsigned char>(t_off + Workspace::aligned(nT * sizeof(G1Xyzz)));
+  uint32_t* err = reinterpret_cast<uint32_t*>(blk);
+  G1Xyzz* Tg = reinterpret_cast<G1Xyzz*>(blk + t_off);
+  uint8_t* dig = ws->carve<uint8_t>(dig_bytes);
+  G1Aff* pts = ws->carve<G1Aff>(pts_bytes / sizeof(G1Aff));
+  if (!d_offsets) {  // one MSM of max_terms terms (msm_run_impl's small path): offsets {0, max_terms}
+    if (count != 1) return SV_ERR_ARG;
+    uint64_t* hoff = reinterpret_cast<uint64_t*>(ws->pinned + Workspace::aligned(back));
+    hoff[0] = 0;
+    hoff[1] = max_terms;
+    uint64_t* doff = ws->carve<uint64_t>(2);
+    SV_HIP(hipMemcpyAsync(doff, hoff, 16, hipMemcpyHostToDevice, st));
+    d_offsets = doff;
+  }
+  SV_HIP(hipMemsetAsync(err, 0, 4, st));
+  hipLaunchKernelGGL(k_batch_prep, dim3((uint32_t)count, (uint32_t)((max_terms + kThreads - 1) / kThreads)),
+                     dim3(kThreads), 0, st, static_cast<const G1Aff*>(d_bases), static_cast<const Fr*>(d_scalars),
+                     d_offsets, nullptr, scalar_form == SV_MONTGOMERY ? 1 : 0, (uint32_t)max_terms, dig, pts, err,
+                     nullptr, (uint64_t)0, base_form == SV_MONTGOMERY ? 1 : 0);
+  hipLaunchKernelGGL(k_batch_windows_q, dim3((uint32_t)count, (uint32_t)kQW), dim3(64), 0, st, d_offsets, nullptr,
+                     (uint32_t)max_terms, dig, pts, Tg);
+  SV_HIP(hipGetLastError());
+  SV_HIP(hipMemcpyAsync(ws->pinned, blk, back, hipMemcpyDeviceToHost, st));
+  SV_HIP(hipStreamSynchronize(st));
+  uint32_t ev;
+  memcpy(&ev, ws->pinned, 4);
+  if (ev & 1u) {
+    set_error("msm_batch: base coordinate not reduced mod p");
+    return SV_ERR_ARG;
+  }
+  if (ev & 2u) {
+    set_error("msm_batch: scalar not reduced (>= r)");
+    return SV_ERR_ARG;
+  }
+  // the window sums are canonical Montgomery XYZZ: host::Xyzz has the same bytes
+  const host::Xyzz* T = reinterpret_cast<const host::Xyzz*>(ws->pinned + t_off);
+  for (size_t k = 0; k < count; k++) {
+    const host::Xyzz* t = T + k * kQW;
+    host::Xyzz acc = t[kQW - 1];
+    for (int w = kQW - 2; w >= 0; w--) {
+      for (int i = 0; i < kQC; i++) acc = host::x_dbl(acc);
+      acc = host::x_add(acc, t[w]);
+    }
+    out[k] = acc;
+  }
+  return SV_OK;
+}
 
 }  // namespace sv
 

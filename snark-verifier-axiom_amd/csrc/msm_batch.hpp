@@ -16,6 +16,13 @@ int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t*
                      size_t count, size_t max_terms, int form, int device, hipStream_t stream, void* d_out,
                      const uint32_t* d_bidx = nullptr, uint64_t table_len = 0, int base_form = 0);
 int msm_batch_window_bits(size_t max_terms);
+// A few small MSMs (each at most 256 terms, the largest max_terms) with the window sums on the device
+// and the window Horner on the host: out[k] = MSM k as a host XYZZ point (Montgomery).  Scalars in
+// scalar_form, bases in base_form.  Synchronous on `stream`.
+namespace host { struct Xyzz; }
+int msm_batch_windows_host(const void* d_bases, const void* d_scalars, const uint64_t* d_offsets, size_t count,
+                           size_t max_terms, int scalar_form, int base_form, int device, hipStream_t stream,
+                           host::Xyzz* out);
 
 // Precomputed base tables: every row P expanded to its window multiples 2^(8 w) P (affine,
 // Montgomery) so that table-backed MSMs need one bucket set and no window Horner.

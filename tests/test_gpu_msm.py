@@ -322,3 +322,32 @@ def test_optional_pipeline_paths(gpu, oracle_cpp, monkeypatch, opt, chain):
         St = torch.from_numpy(S.view(np.int64)).to(dev)
         assert dv.msm(Bt, St, svgpu.SV_CANONICAL) == exp, (opt, n, "device")  # the split path's input
         assert svgpu.msm_arrays(B, S) == exp, (opt, n, "host")
+
+
+@pytest.mark.parametrize("small", ["0", "1"])
+@pytest.mark.parametrize("n", [1, 2, 3, 31, 64, 65, 200, 256, 257])
+def test_small_msm_path_vs_pipeline(gpu, oracle_cpp, n, small, monkeypatch):
+    """MSMs of at most 256 terms take the small path (round 5: window sums on the device, the window
+    Horner on the host, msm_batch.hip msm_batch_windows_host); SVGPU_SMALL_MSM=0 keeps the pipeline.
+    Both give the reference Pippenger's point -- host-fed in both forms and device-resident -- with a
+    zero scalar, an identity base, a repeated point and a cancelling pair mixed in."""
+    import svgpu
+    from svgpu import device as dv, encoding as enc
+    monkeypatch.setenv("SVGPU_SMALL_MSM", small)
+    B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=13 * n).copy()
+    S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=13 * n).copy()
+    if n >= 4:
+        S[0] = 0                      # a zero scalar
+        B[1] = 0                      # the identity base (0, 0)
+        B[2], S[2] = B[3], S[3]       # a repeated point (same bucket: the doubling case)
+    if n >= 6:
+        B[5] = enc.bases_array([b.g1_neg(enc.g1_from_limbs(B[4]))])[0]
+        S[5] = S[4]                   # P and -P with equal scalars cancel
+    exp = _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
+    assert svgpu.msm_arrays(B, S, svgpu.SV_CANONICAL) == exp
+    Bm = enc.bases_array([enc.g1_from_limbs(r) for r in B], svgpu.SV_MONTGOMERY)
+    Sm = enc.scalars_array([enc.limbs_to_int(r) for r in S], svgpu.SV_MONTGOMERY)
+    assert svgpu.msm_arrays(Bm, Sm, svgpu.SV_MONTGOMERY) == exp
+    Bd = torch.from_numpy(B.view(np.int64)).to(gpu)
+    Sd = torch.from_numpy(S.view(np.int64)).to(gpu)
+    assert dv.msm(Bd, Sd, svgpu.SV_CANONICAL) == exp

@@ -428,10 +428,10 @@ struct BucketSmem {
   uint16_t lst[2 * kQMaxTerms];
 };
 
-__device__ __forceinline__ void bucket_window(BucketSmem& sm, uint32_t k, uint32_t w, const uint64_t* __restrict__ off,
-                                              const uint32_t* __restrict__ ids, uint32_t max_terms,
-                                              const uint8_t* __restrict__ dig, const G1Aff* __restrict__ pts,
-                                              G1Xyzz* __restrict__ Sb) {
+// quad b of the wave returns S_b (quad form, 2p domain) of window w of batch entry k
+__device__ __forceinline__ Fq bucket_sum_q(BucketSmem& sm, uint32_t k, uint32_t w, const uint64_t* __restrict__ off,
+                                           const uint32_t* __restrict__ ids, uint32_t max_terms,
+                                           const uint8_t* __restrict__ dig, const G1Aff* __restrict__ pts) {
   const uint32_t lane = threadIdx.x;
   const uint32_t id = ids ? ids[k] : k;
   const uint32_t m = (uint32_t)(off[id + 1] - off[id]);
@@ -473,7 +473,48 @@ __device__ __forceinline__ void bucket_window(BucketSmem& sm, uint32_t k, uint32
   Fq q[4] = {acc.X, acc.Y, acc.ZZ, acc.ZZZ};
   quad::transpose(q, c);  // lane c: coordinate c of the quad's four partial sums
   const Fq s01 = quad::add_2p(q[0], q[1], c), s23 = quad::add_2p(q[2], q[3], c);
-  quad::st(Sb + ((size_t)k * kQB + b) * kQW + w, c, fe_canon2p(quad::add_2p(s01, s23, c)));
+  return quad::add_2p(s01, s23, c);
+}
+
+__device__ __forceinline__ void bucket_window(BucketSmem& sm, uint32_t k, uint32_t w, const uint64_t* __restrict__ off,
+                                              const uint32_t* __restrict__ ids, uint32_t max_terms,
+                                              const uint8_t* __restrict__ dig, const G1Aff* __restrict__ pts,
+                                              G1Xyzz* __restrict__ Sb) {
+  const Fq S = bucket_sum_q(sm, k, w, off, ids, max_terms, dig, pts);
+  const int c = threadIdx.x & 3, b = threadIdx.x >> 2;
+  quad::st(Sb + ((size_t)k * kQB + b) * kQW + w, c, fe_canon2p(S));
+}
+
+// Window sums for a host Horner (round 5, msm_batch_windows_host): one wave per (MSM, window).  The
+// bucket sums S_b stay in quad form (bucket_sum_q), and sum_b (b + 1) S_b = sum_k 2^k U_k with U_k
+// the sum of the S_b whose digit magnitude d = b + 1 has bit k set -- eight buckets each for
+// k < 4 (a quad adds two, then two levels inside its 16-lane row), U_4 = S_15 -- so the window needs
+// 3 quad additions after the bucket chains where k_batch_windows_q's scan + tree needs 8 (and its
+// unrolled straight-line code, fetched once per wave, cost 285 us for create_proof's two 64-term
+// MSMs at one wave per CU).  The host places U_k at exponent 5 w + k of one Horner.
+constexpr int kUPerWin = kQC;  // U_0 .. U_4
+__global__ void __launch_bounds__(64) k_batch_uwin(const uint64_t* __restrict__ off, uint32_t max_terms,
+                                                   const uint8_t* __restrict__ dig, const G1Aff* __restrict__ pts,
+                                                   G1Xyzz* __restrict__ U) {
+  __shared__ BucketSmem sm;
+  __shared__ Fq sb[kQB][4];
+  const uint32_t k = blockIdx.x, w = blockIdx.y;
+  const int c = threadIdx.x & 3, b = threadIdx.x >> 2;
+  const Fq S = bucket_sum_q(sm, k, w, off, nullptr, max_terms, dig, pts);
+  sb[b][c] = S;
+  __syncthreads();
+  const int kk = b >> 2, j = b & 3;  // quad (kk, j): members j and j + 4 of U_kk
+  auto member = [&](int i) {         // the i-th magnitude with bit kk set, as its bucket index
+    return ((((i >> kk) << (kk + 1)) | (1 << kk) | (i & ((1 << kk) - 1))) - 1);
+  };
+  Fq u = quad::add_2p(sb[member(j)][c], sb[member(j + 4)][c], c);
+  Fq o = quad::down(u, 8);  // (every shuffle runs on every lane; the additions are quad-uniform)
+  if (j < 2) u = quad::add_2p(u, o, c);
+  o = quad::down(u, 4);
+  if (j == 0) u = quad::add_2p(u, o, c);
+  G1Xyzz* dst = U + ((size_t)k * kQW + w) * kUPerWin;
+  if (j == 0) quad::st(dst + kk, c, fe_canon2p(u));
+  if (b == kQB - 1) quad::st(dst + 4, c, fe_canon2p(S));  // U_4 = S_15 (magnitude 16)
 }
 
 // Bounded wait for a window's bucket sums (fused kernel): a wave that never sees the flag (a bug,
@@ -1059,8 +1100,8 @@ uint64_t msm_batch_fused_redone() { return g_fused_redone.load(std::memory_order
 // kQMaxTerms terms -- KzgAs::create_proof's two r^i MSMs (accumulation.rs:177-192), a native
 // verifier's per-proof MSMs -- is bound by its serial tail: the Horner over the 26 windows of a
 // 128-bit GLV half (130 doublings) is ~475 dependent product levels on one GPU wave, ~0.25 ms, but
-// ~20 us on the host (host_ec.hpp).  The device forms every window sum T_w (k_batch_prep +
-// k_batch_windows_q: ~16 quad-operation levels), one copy brings them back, the host combines them.
+// ~40 us on the host (host_ec.hpp).  The device forms each window's partial sums U_k (k_batch_prep
+// + k_batch_uwin), one copy brings them back, the host combines them.
 // d_offsets = nullptr: one MSM of max_terms terms.
 int msm_batch_windows_host(const void* d_bases, const void* d_scalars, const uint64_t* d_offsets, size_t count,
                            size_t max_terms, int scalar_form, int base_form, int device, hipStream_t stream,
@@ -1074,7 +1115,7 @@ int msm_batch_windows_host(const void* d_bases, const void* d_scalars, const uin
   if (!lease.ok()) return SV_ERR_DEVICE;
   Workspace* ws = lease.get();
   hipStream_t st = ws->stream;
-  const size_t nT = count * kQW;
+  const size_t nT = count * kQW * kUPerWin;
   const size_t dig_bytes = count * kQW * 2 * max_terms;
   const size_t pts_bytes = count * 2 * max_terms * sizeof(G1Aff);
   const size_t t_off = 256;  // the error word, then the window sums: ONE copy back
@@ -1101,7 +1142,7 @@ int msm_batch_windows_host(const void* d_bases, const void* d_scalars, const uin
                      dim3(kThreads), 0, st, static_cast<const G1Aff*>(d_bases), static_cast<const Fr*>(d_scalars),
                      d_offsets, nullptr, scalar_form == SV_MONTGOMERY ? 1 : 0, (uint32_t)max_terms, dig, pts, err,
                      nullptr, (uint64_t)0, base_form == SV_MONTGOMERY ? 1 : 0);
-  hipLaunchKernelGGL(k_batch_windows_q, dim3((uint32_t)count, (uint32_t)kQW), dim3(64), 0, st, d_offsets, nullptr,
+  hipLaunchKernelGGL(k_batch_uwin, dim3((uint32_t)count, (uint32_t)kQW), dim3(64), 0, st, d_offsets,
                      (uint32_t)max_terms, dig, pts, Tg);
   SV_HIP(hipGetLastError());
   SV_HIP(hipMemcpyAsync(ws->pinned, blk, back, hipMemcpyDeviceToHost, st));
@@ -1116,17 +1157,18 @@ int msm_batch_windows_host(const void* d_bases, const void* d_scalars, const uin
     set_error("msm_batch: scalar not reduced (>= r)");
     return SV_ERR_ARG;
   }
-  // the window sums are canonical Montgomery XYZZ: host::Xyzz has the same bytes
-  const host::Xyzz* T = reinterpret_cast<const host::Xyzz*>(ws->pinned + t_off);
-  for (size_t k = 0; k < count; k++) {
-    const host::Xyzz* t = T + k * kQW;
-    host::Xyzz acc = t[kQW - 1];
-    for (int w = kQW - 2; w >= 0; w--) {
-      for (int i = 0; i < kQC; i++) acc = host::x_dbl(acc);
-      acc = host::x_add(acc, t[w]);
+  // the partial sums are canonical Montgomery XYZZ (host::Xyzz has the same bytes); U_k of window w
+  // sits at exponent 5 w + k: one Horner over the 130 exponents per MSM, the MSMs on the host pool
+  const host::Xyzz* U = reinterpret_cast<const host::Xyzz*>(ws->pinned + t_off);
+  constexpr int kTop = kQW * kUPerWin - 1;
+  host_parallel_for(count, 1, [&](size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; k++) {
+      const host::Xyzz* u = U + k * kQW * kUPerWin;
+      host::Xyzz acc = u[kTop];
+      for (int e = kTop - 1; e >= 0; e--) acc = host::x_add(host::x_dbl(acc), u[e]);
+      out[k] = acc;
     }
-    out[k] = acc;
-  }
+  });
   return SV_OK;
 }
 

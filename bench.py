@@ -32,8 +32,18 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0            # MI355X spec (MI355X_MICROARCH.md)
-MAC_PEAK = 32 * 256 * 2.4e9      # v_mad_u64_u32: 32 / clk / CU (quarter rate x 4 SIMD-32), 256 CUs, 2.4 GHz
+# v_mad_u64_u32 issue peak: one wave instruction per 4 clocks per SIMD (16 lanes / clk) x 4 SIMDs x 256
+# CUs x 2.4 GHz = 64 lane-mads / clk / CU.  tools/ubench_issue.hip (round 5) measured 4.25 clocks per
+# mad with 16 independent chains at 4 waves / SIMD (60.2 / clk / CU) and showed that every other VALU
+# instruction takes issue time of its own (2-3.8 clocks): the bucket chain is bound by VALU issue, of
+# which its mads are ~55 %.  (Rounds 1-4 used 32 / clk / CU, which the kernel appeared to exceed.)
+MAC_PEAK = 64 * 256 * 2.4e9
+MAC_PEAK_MEASURED = 64 * 4 / 4.25 * 256 * 2.4e9
 MACS_PER_FPMUL = 136             # 8-limb CIOS: 64 + 64 + 8
+# v_mad_u64_u32 per bucket entry that k_accumulate<false, true, 1> (the 29-bit chain) issues on its
+# common path (no segment end, no doubling): tools/isa_count.py over the compiler's assembly
+# (81 + 81 per product, 45 + 81 per square, 243 for the fused Y3 pair, + 36)
+MADS_PER_ENTRY_R29 = 1503
 BYTES_PER_POINT = 96             # 64 B affine base + 32 B scalar, read once
 # Decider algorithmic work: Fq products of ONE decide, COUNTED by instrumenting the C++
 # restatements (oracle/cpu/bn254_ref.cpp; both pinned by tests/test_oracle_cpp.py):
@@ -45,6 +55,9 @@ BYTES_PER_POINT = 96             # 64 B affine base + 32 B scalar, read once (SU
 #    exponentiation): an upper bound, reported for comparison.
 FPMUL_H2C_COUNTED = 24710
 FPMUL_RESTATEMENT = 57538
+# of FPMUL_H2C_COUNTED, the two G2 line preparations (G2Prepared::from inside every decide,
+# decider.rs:64), which the GPU decider caches per deciding key (or_count_h2c_prepare)
+FPMUL_H2C_LINE_PREP = 5366
 
 
 def parse():
@@ -452,7 +465,23 @@ def main():
             traffic = json.load(open(prof)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    macs = entries * 10 * MACS_PER_FPMUL  # one mixed XYZZ add (8M + 2S) per bucket entry
+    macs = entries * 10 * MACS_PER_FPMUL  # one mixed XYZZ add (8M + 2S) per bucket entry, 8x32-bit work
+    issued = entries * MADS_PER_ENTRY_R29  # what the 29-bit chain issues
+    # VALU issue of k_accumulate from the round's SQ pass (profiles/*_sq_counters.json): wave
+    # instructions per dispatch x 4 clocks over the launch's SIMD-clocks (live kernel time)
+    valu = None
+    sqf = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_sq_counters.json"))
+    if sqf:
+        try:
+            sqd = json.load(open(os.path.join(ROOT, "profiles", sqf[-1])))
+            ka = next(v for k, v in sqd.items() if k.startswith("k_accumulate") and "SQ_INSTS_VALU" in v)
+            vi = ka["SQ_INSTS_VALU"]
+            valu = {"source": "profiles/" + sqf[-1], "valu_wave_insts_per_dispatch": vi,
+                    "valu_per_entry_wave": vi / (entries / 64.0),
+                    "int64_share": ka.get("SQ_INSTS_VALU_INT64", 0) / vi if vi else None,
+                    "issue_frac_4clk": vi * 4 / (acc_avg_ms * 1e-3 * 2.4e9 * 1024)}
+        except (StopIteration, KeyError, ValueError, OSError):
+            valu = None
     c_ref = ref_window(n)
     W_ref = -(-256 // c_ref)
     ref_macs = (W_ref * n * 11 + W_ref * 2 * ((1 << c_ref) - 1) * 16) * MACS_PER_FPMUL
@@ -498,7 +527,12 @@ def main():
             "int_mac": {
                 "achieved": dn * FPMUL_H2C_COUNTED * MACS_PER_FPMUL / (np.mean(dec_kernel_ms) * 1e-3),
                 "frac": dn * FPMUL_H2C_COUNTED * MACS_PER_FPMUL / (np.mean(dec_kernel_ms) * 1e-3) / MAC_PEAK,
-                "unit": "MAC/s (v_mad_u64_u32), work = accumulators x h2c_restatement_counted Fq products x 136",
+                "frac_without_line_prep": dn * (FPMUL_H2C_COUNTED - FPMUL_H2C_LINE_PREP) * MACS_PER_FPMUL
+                                          / (np.mean(dec_kernel_ms) * 1e-3) / MAC_PEAK,
+                "peak": MAC_PEAK,
+                "unit": "MAC/s (v_mad_u64_u32), work = accumulators x h2c_restatement_counted Fq products x 136; "
+                        "frac_without_line_prep drops the %d products of the two G2 line preparations the kernel "
+                        "caches per key" % FPMUL_H2C_LINE_PREP,
             },
         },
         "breakdown_ms": {k: round(stats[k], 4) for k in
@@ -517,17 +551,26 @@ def main():
             "kernel_avg_ms": acc_avg_ms,
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "launches_per_msm": groups,
-            "note": "path is VALU integer-multiply bound, not HBM: see int_mac",
+            "traffic_over_algorithmic": (traffic / bytes_per_launch) if traffic else None,
+            "note": "path is VALU-issue bound (integer multiply + carry handling), not HBM: see int_mac",
         },
         "int_mac": {
-            "kernel_achieved": macs / (acc_span_ms * 1e-3),
-            "kernel_frac": macs / (acc_span_ms * 1e-3) / MAC_PEAK,
+            "kernel_issued_mads_per_entry": MADS_PER_ENTRY_R29,
+            "kernel_achieved": issued / (acc_span_ms * 1e-3),
+            "kernel_frac": issued / (acc_span_ms * 1e-3) / MAC_PEAK,
+            "kernel_frac_of_measured_peak": issued / (acc_span_ms * 1e-3) / MAC_PEAK_MEASURED,
+            "equiv32_achieved": macs / (acc_span_ms * 1e-3),
+            "equiv32_frac": macs / (acc_span_ms * 1e-3) / MAC_PEAK,
             "kernel_time": "accumulate span (first k_accumulate start to last end) %.4f ms; launches' own "
                            "durations sum to %.4f ms" % (acc_span_ms, acc_sum_ms),
             "msm_achieved_ref_work": ref_macs / (elapsed / args.steps),
             "msm_frac_ref_work": ref_macs / (elapsed / args.steps) / MAC_PEAK,
             "peak": MAC_PEAK,
-            "unit": "MAC/s (v_mad_u64_u32)",
+            "peak_measured": MAC_PEAK_MEASURED,
+            "valu_issue": valu,
+            "unit": "MAC/s (v_mad_u64_u32).  kernel_*: the mads the 29-bit chain issues (tools/isa_count.py); "
+                    "equiv32_*: the 8x32-bit work it replaces (10 products x 136 per entry); peak: one wave "
+                    "mad per 4 clocks per SIMD, peak_measured: tools/ubench_issue.hip",
         },
     }
 

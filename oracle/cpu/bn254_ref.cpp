@@ -912,6 +912,22 @@ uint64_t or_count_decide_fpmul_h2c(const uint64_t* g2, const uint64_t* s_g2, con
   return g_fq_muls;
 }
 
+// The part of or_count_decide_fpmul_h2c spent in the two G2 line preparations (G2Prepared::from
+// inside decide, decider.rs:64), which the GPU decider caches per deciding key instead: the
+// roofline's work count without it is the difference.
+uint64_t or_count_h2c_prepare(const uint64_t* g2, const uint64_t* s_g2) {
+  init_consts();
+  G2A q1 = load_g2(g2), q2 = load_g2(s_g2);
+  q2.y = f2n(q2.y);
+  g_fq_muls = 0;
+  g_count_on = true;
+  const std::vector<Line> l1 = h2c::prepare(q1), l2 = h2c::prepare(q2);
+  g_count_on = false;
+  (void)l1;
+  (void)l2;
+  return g_fq_muls;
+}
+
 // KzgAs::create_proof without blind: lhs = sum r^i lhs_i, rhs = sum r^i rhs_i (naive MSMs, as
 // NativeLoader evaluates them).  r canonical.
 int or_accumulate(const uint64_t* lhs, const uint64_t* rhs, size_t n, const uint64_t* r, uint64_t* out_lhs,

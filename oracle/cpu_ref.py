@@ -31,6 +31,8 @@ def lib():
         L.or_count_decide_fpmul.restype = c_uint64
         L.or_count_decide_fpmul_h2c.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
         L.or_count_decide_fpmul_h2c.restype = c_uint64
+        L.or_count_h2c_prepare.argtypes = [c_void_p, c_void_p]
+        L.or_count_h2c_prepare.restype = c_uint64
         L.or_accumulate.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p]
         L.or_gen_scalars.argtypes = [c_uint64, c_uint64, c_size_t, c_void_p]
         L.or_gen_scalars.restype = None
@@ -88,6 +90,13 @@ def count_decide_fpmul_h2c(g2: np.ndarray, s_g2: np.ndarray, lhs_row, rhs_row):
     n = int(lib().or_count_decide_fpmul_h2c(g2.ctypes.data, s_g2.ctypes.data, l.ctypes.data, r.ctypes.data,
                                             gt.ctypes.data))
     return n, gt
+
+
+def count_h2c_prepare(g2: np.ndarray, s_g2: np.ndarray) -> int:
+    """The Fq products of count_decide_fpmul_h2c spent in the two G2 line preparations
+    (G2Prepared::from inside decide, decider.rs:64), which the GPU decider caches per key."""
+    g2, s_g2 = _c(g2), _c(s_g2)
+    return int(lib().or_count_h2c_prepare(g2.ctypes.data, s_g2.ctypes.data))
 
 
 def accumulate(lhs, rhs, r: np.ndarray):

@@ -226,6 +226,41 @@ SV29_HD F29<M> mul_sum3(const F29<M>& a0, const F29<M>& b0, const F29<M>& a1, co
 }
 #undef SV29_REDUCE_COLUMN
 
+// a b / R' mod p like mul (inputs below 12p -> output below 2p), scheduled for the latency of ONE
+// wave (the decider's lane products, round 5): the 81 partial products go to 17 separate 64-bit
+// column accumulators (consecutive mads are independent), then 9 reduction steps, each a short
+// dependent chain (m from the column's low word, the m p_0 mad, the carry into the next column)
+// with its 8 other mads off the chain.  A column collects at most 9 + 9 products below 2^58 plus a
+// carry below 2^35: below 2^63.
+template <class M>
+SV29_HD F29<M> mul_ilp(const F29<M>& a, const F29<M>& b) {
+  uint64_t c[2 * L - 1];
+#pragma unroll
+  for (int k = 0; k < 2 * L - 1; k++) c[k] = 0;
+#pragma unroll
+  for (int i = 0; i < L; i++)
+#pragma unroll
+    for (int j = 0; j < L; j++) c[i + j] = mad(a.v[i], b.v[j], c[i + j]);
+#pragma unroll
+  for (int k = 0; k < L; k++) {
+    const uint32_t m = ((uint32_t)c[k] * M::NP) & MASK;
+    c[k] = mad(m, M::kp(1, 0), c[k]);  // the low 29 bits are now zero
+    c[k + 1] += c[k] >> 29;
+#pragma unroll
+    for (int j = 1; j < L; j++) c[k + j] = mad(m, M::kp(1, j), c[k + j]);
+  }
+  F29<M> t;
+  uint64_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < L - 1; i++) {
+    const uint64_t x = c[L + i] + carry;
+    t.v[i] = (uint32_t)x & MASK;
+    carry = x >> 29;
+  }
+  t.v[L - 1] = (uint32_t)carry;
+  return t;
+}
+
 // a - b + K p, normalized (b below K p; the result is below bound(a) + K p)
 template <int K, class M>
 SV29_HD F29<M> sub(const F29<M>& a, const F29<M>& b) {

@@ -75,6 +75,8 @@ static int run_ops(bool fq) {
     F29<M> a = below<M>(12, mode), b = below<M>(12, (mode + 1) % 3), c = below<M>(12, mode), d = below<M>(12, (mode + 2) % 3);
     printf("mul");
     pr(a), pr(b), pr(mul(a, b));
+    printf("\nmul_ilp");
+    pr(a), pr(b), pr(mul_ilp(a, b));
     printf("\nsqr");
     pr(a), pr(sqr(a));
     printf("\nmul_sum2");

@@ -50,12 +50,12 @@ def test_field_ops_values_and_bounds(f29, field):
                 continue
             assert r < 2 * P, line
             assert r % P == (a0 * b0 + a1 * b1 + a2 * b2) * RINV % P, line
-        elif op in ("mul", "sqr", "mul_sum2"):
+        elif op in ("mul", "mul_ilp", "sqr", "mul_sum2"):
             bound_in = 12 * P if op != "mul_sum2" else 9 * P
             ins, r = v[:-1], v[-1]
             if any(x >= bound_in for x in ins):
                 continue  # outside the stated contract: not checked
-            if op == "mul":
+            if op in ("mul", "mul_ilp"):
                 want = ins[0] * ins[1]
             elif op == "sqr":
                 want = ins[0] * ins[0]
@@ -93,7 +93,7 @@ def test_field_ops_values_and_bounds(f29, field):
         elif op == "to_r32":
             a, r = v
             assert r < P and r == a * pow(32, -1, P) % P, line
-    assert counts.get("mul", 0) >= 3000 and counts.get("to_r32", 0) >= 3000 and counts.get("mul_sum3", 0) >= 3000
+    assert counts.get("mul", 0) >= 3000 and counts.get("mul_ilp", 0) >= 3000 and counts.get("to_r32", 0) >= 3000 and counts.get("mul_sum3", 0) >= 3000
     assert counts.get("zero6", 0) >= (3006 if field == "fq" else 0)
 
 

@@ -104,3 +104,16 @@ def test_decide_fpmul_h2c_count_is_the_bench_denominator_and_gt_agrees(oracle_cp
         assert (gt == gts[i]).all()
     src = open(os.path.join(ROOT, "bench.py")).read()
     assert counts == {int(re.search(r"FPMUL_H2C_COUNTED = (\d+)", src).group(1))}
+
+
+def test_h2c_line_prep_count_is_the_bench_constant():
+    """bench.py's FPMUL_H2C_LINE_PREP: the Fq products of the two G2 line preparations inside one
+    h2c decide (G2Prepared::from, decider.rs:64), which the GPU decider caches per deciding key; the
+    roofline's frac_without_line_prep drops them."""
+    import re
+    from oracle import cpu_ref
+    g2, sg2, _ = b.gen_decider_case(2)
+    cnt = cpu_ref.count_h2c_prepare(np.frombuffer(b.g2_bytes(g2), np.uint64), np.frombuffer(b.g2_bytes(sg2), np.uint64))
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert int(re.search(r"FPMUL_H2C_LINE_PREP = (\d+)", src).group(1)) == cnt
+    assert cnt < int(re.search(r"FPMUL_H2C_COUNTED = (\d+)", src).group(1))

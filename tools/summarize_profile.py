@@ -63,6 +63,28 @@ if os.path.exists(cal_csv):
               "| pattern | FETCH_SIZE KiB | known MB | factor (known / FETCH_SIZE) |", "|---|---|---|---|"]
     for k, v in calib.items():
         lines.append("| %s | %.0f | %.1f | %.3f |" % (k, v["fetch_kib"], v["known_bytes"] / 1e6, v["factor"] or 0))
+# SQ instruction / cycle counters (round 5: sq_valu, sq_wait passes), per dispatch, for the two
+# dominant kernels; per-wave figures divide by SQ_WAVES
+sq = {}
+for sub in ("sq_valu", "sq_wait"):
+    f = os.path.join(src, sub, "run_counter_collection.csv")
+    if not os.path.exists(f):
+        continue
+    acc = defaultdict(lambda: defaultdict(list))
+    for r in csv.DictReader(open(f)):
+        acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for k, d in acc.items():
+        sq.setdefault(k, {}).update({c: sum(v) / len(v) for c, v in d.items()})
+if sq:
+    lines += ["", "## SQ counters per dispatch (separate --pmc passes; chip totals, per wave = / SQ_WAVES)", ""]
+    for k in [k for k in sq if k.startswith("k_accumulate") or k.startswith("k_decide_wg")]:
+        d = sq[k]
+        waves = d.get("SQ_WAVES", 0) or 1
+        lines += ["### " + k, "", "| counter | per dispatch | per wave |", "|---|---|---|"]
+        for c in sorted(d):
+            lines.append("| %s | %.4g | %.4g |" % (c, d[c], d[c] / waves))
+        lines.append("")
+    json.dump(sq, open(os.path.join(dst, f"{tag}_sq_counters.json"), "w"), indent=1)
 open(os.path.join(dst, f"{tag}_kernel_stats.md"), "w").write("\n".join(lines) + "\n")
 acc_key = next((k for k in pmc["FETCH_SIZE"] if k.startswith("k_accumulate")), None)  # k_accumulate<false> since r03
 acc_f = pmc["FETCH_SIZE"].get(acc_key) if acc_key else None

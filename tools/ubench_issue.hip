@@ -58,6 +58,36 @@ __global__ void __launch_bounds__(256, 4) k_mix(uint64_t* out, int iters) {
   out[tid] = s;
 }
 
+// no mads: NA independent v_add_u32 per iteration (the VALU issue rate of a plain 32-bit op), or
+// 16 independent mad chains (is 8 chains x 4 waves enough to reach the mad issue rate?)
+template <int MODE>
+__global__ void __launch_bounds__(256, 4) k_alt(uint64_t* out, int iters) {
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t acc[16];
+  uint32_t a[16], x[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    acc[j] = tid + j;
+    a[j] = tid * 3 + j;
+    x[j] = tid * 7 + j;
+  }
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      if constexpr (MODE == 0) {
+        asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[j]) : "v"(a[j]));
+      } else {
+        asm volatile("v_mad_u64_u32 %0, s[0:1], %1, %2, %0" : "+v"(acc[j]) : "v"(a[j]), "v"(x[j]) : "s0", "s1");
+        asm volatile("v_mad_u64_u32 %0, s[0:1], %1, %2, %0" : "+v"(acc[j + 8]) : "v"(a[j + 8]), "v"(x[j + 8]) : "s0", "s1");
+      }
+    }
+  }
+  uint64_t s = 0;
+#pragma unroll
+  for (int j = 0; j < 16; j++) s += acc[j] + x[j];
+  out[tid] = s;
+}
+
 template <typename K>
 static float run(const char* name, K kern, uint64_t* d, double others_per_mad, float base) {
   hipEvent_t e0, e1;
@@ -99,5 +129,9 @@ int main() {
   run("mad + 1 add_co/addc", k_mix<6, 1>, (uint64_t*)d, 2, base);
   run("mad + 1 bfe_u32", k_mix<7, 1>, (uint64_t*)d, 1, base);
   run("mad + 8 add_u32", k_mix<1, 8>, (uint64_t*)d, 8, base);
+  // per 'mad' slot below: k_alt<0> issues 8 adds per iteration (reported as 'mads'), k_alt<1> 16 mads
+  run("add_u32 only (as mads)", k_alt<0>, (uint64_t*)d, 0, 0);
+  const float m16 = run("16 mad chains (x2)", k_alt<1>, (uint64_t*)d, 0, 0);
+  printf("16 mad chains: %.2f cycles per mad\n", m16 * 1e-3 * 2.4e9 * 1024 / (8192.0 * 256 / 64 * 1000 * 16));
   return 0;
 }

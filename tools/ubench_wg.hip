@@ -3,6 +3,7 @@
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -Isnark-verifier-axiom_amd/csrc tools/ubench_wg.hip \
 //          snark-verifier-axiom_amd/csrc/runtime.cpp -o tools/ubench_wg
 #include "../snark-verifier-axiom_amd/csrc/decider.hip"
+#include "../snark-verifier-axiom_amd/csrc/field29.hpp"
 
 #include <cstdio>
 #include <vector>
@@ -41,8 +42,18 @@ __global__ void __launch_bounds__(256) k_bench(int op, int iters, unsigned long 
   }
 }
 
+// round 5: a product on 8 x 32-bit words computed with field29.hpp's mul_ilp (x R' domain: the words
+// are converted to 9 x 29-bit limbs and back) -- timing only, the domain is not the slots' one
+__device__ __forceinline__ Fq mul29w(const Fq& a, const Fq& b) {
+  const r29::F x = r29::from_words(a.v), y = r29::from_words(b.v);
+  Fq r;
+  r29::to_words(r29::mul_ilp(x, y), r.v);
+  return r;
+}
+
 // w_mul with parts switched off (mode bits): 1 no product, 2 no lane sum, 4 no lz_reduce,
-// 8 no barrier, 16 no LDS operand loads (registers instead); the same code as wg::w_mul otherwise
+// 8 no barrier, 16 no LDS operand loads (registers instead), 32 the product by mul29w; the same
+// code as wg::w_mul otherwise
 __device__ __forceinline__ void w_mul_dbg(const wg::WLane& L, Fq2* __restrict__ dst, const Fq2* a, const Fq2* b,
                                           int mode) {
   using namespace wg;
@@ -58,7 +69,7 @@ __device__ __forceinline__ void w_mul_dbg(const wg::WLane& L, Fq2* __restrict__ 
       ax = ld_fq((q & 1) ? &a[L.mi].c1 : &a[L.mi].c0);
       by = ld_fq((q == 1 || q == 2) ? &b[L.mjj].c1 : &b[L.mjj].c0);
     }
-    Fq v = (mode & 1) ? ax : ax * by;
+    Fq v = (mode & 1) ? ax : ((mode & 32) ? mul29w(ax, by) : fe_mul_lazy(ax, by));
     if (!L.mact) v = Fq::zero();
     const Fq nv = fq_neg2p(v);
     Lz re, im;
@@ -110,6 +121,20 @@ __global__ void k_fqmul(int iters, unsigned long long* cycles, uint32_t* sink) {
   const Fq y = x;
   const unsigned long long t0 = clock64();
   for (int i = 0; i < iters; i++) x = x * y;
+  const unsigned long long t1 = clock64();
+  if (threadIdx.x == 0) *cycles = t1 - t0;
+  sink[threadIdx.x] = x.v[0];
+}
+
+__global__ void k_fqmul_var(int var, int iters, unsigned long long* cycles, uint32_t* sink) {
+  Fq x = Fq::one();
+  x.v[0] ^= threadIdx.x;
+  const Fq y = x;
+  const unsigned long long t0 = clock64();
+  if (var == 0)
+    for (int i = 0; i < iters; i++) x = fe_mul_lazy(x, y);
+  else
+    for (int i = 0; i < iters; i++) x = mul29w(x, y);
   const unsigned long long t1 = clock64();
   if (threadIdx.x == 0) *cycles = t1 - t0;
   sink[threadIdx.x] = x.v[0];
@@ -168,7 +193,7 @@ int main() {
     (void)hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
     printf("%-7s %8.1f cycles/op (clock64)\n", names[op], (double)c / iters);
   }
-  for (int mode : {0, 1, 2, 4, 8, 16, 2 | 4, 1 | 2 | 4, 1 | 2 | 4 | 8, 31}) {
+  for (int mode : {0, 32, 1, 2, 4, 8, 16, 2 | 4, 1 | 2 | 4, 1 | 2 | 4 | 8, 31, 32 | 2 | 4}) {
     hipLaunchKernelGGL(k_bench_dbg, dim3(1), dim3(256), 0, 0, mode, 4, dc, ds);
     hipLaunchKernelGGL(k_bench_dbg, dim3(1), dim3(256), 0, 0, mode, iters, dc, ds);
     unsigned long long c = 0;
@@ -179,6 +204,12 @@ int main() {
   unsigned long long c = 0;
   (void)hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
   printf("%-7s %8.1f cycles/op (one wave, dependent Fq products)\n", "fq_mul", (double)c / iters);
+  for (int var = 0; var < 2; var++) {
+    hipLaunchKernelGGL(k_fqmul_var, dim3(1), dim3(64), 0, 0, var, 4, dc, ds);
+    hipLaunchKernelGGL(k_fqmul_var, dim3(1), dim3(64), 0, 0, var, iters, dc, ds);
+    (void)hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
+    printf("%-12s %8.1f cycles/op (one wave, dependent)\n", var ? "mul29w" : "fe_mul_lazy", (double)c / iters);
+  }
   hipLaunchKernelGGL(k_inv, dim3(1), dim3(64), 0, 0, 2, dc, ds);
   hipLaunchKernelGGL(k_inv, dim3(1), dim3(64), 0, 0, 20, dc, ds);
   (void)hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);

@@ -428,8 +428,9 @@ struct BucketSmem {
   uint16_t lst[2 * kQMaxTerms];
 };
 
-// quad b of the wave returns S_b (quad form, 2p domain) of window w of batch entry k
-__device__ __forceinline__ Fq bucket_sum_q(BucketSmem& sm, uint32_t k, uint32_t w, const uint64_t* __restrict__ off,
+// lane 4b + c of the wave returns the sum of every 4th entry of bucket b (from the c-th) of window w
+// of batch entry k: the LDS counting sort of the window's digits, then a chain of mixed additions
+__device__ __forceinline__ G1Xyzz bucket_chain(BucketSmem& sm, uint32_t k, uint32_t w, const uint64_t* __restrict__ off,
                                            const uint32_t* __restrict__ ids, uint32_t max_terms,
                                            const uint8_t* __restrict__ dig, const G1Aff* __restrict__ pts) {
   const uint32_t lane = threadIdx.x;
@@ -470,6 +471,15 @@ __device__ __forceinline__ Fq bucket_sum_q(BucketSmem& sm, uint32_t k, uint32_t 
     if (v >> 15) y = -y;
     acc = xyzz_madd_2p(acc, x, y);
   }
+  return acc;
+}
+
+// quad b of the wave returns S_b (quad form, 2p domain) of window w of batch entry k
+__device__ __forceinline__ Fq bucket_sum_q(BucketSmem& sm, uint32_t k, uint32_t w, const uint64_t* __restrict__ off,
+                                           const uint32_t* __restrict__ ids, uint32_t max_terms,
+                                           const uint8_t* __restrict__ dig, const G1Aff* __restrict__ pts) {
+  const G1Xyzz acc = bucket_chain(sm, k, w, off, ids, max_terms, dig, pts);
+  const int c = threadIdx.x & 3;
   Fq q[4] = {acc.X, acc.Y, acc.ZZ, acc.ZZZ};
   quad::transpose(q, c);  // lane c: coordinate c of the quad's four partial sums
   const Fq s01 = quad::add_2p(q[0], q[1], c), s23 = quad::add_2p(q[2], q[3], c);
@@ -485,36 +495,99 @@ __device__ __forceinline__ void bucket_window(BucketSmem& sm, uint32_t k, uint32
   quad::st(Sb + ((size_t)k * kQB + b) * kQW + w, c, fe_canon2p(S));
 }
 
-// Window sums for a host Horner (round 5, msm_batch_windows_host): one wave per (MSM, window).  The
-// bucket sums S_b stay in quad form (bucket_sum_q), and sum_b (b + 1) S_b = sum_k 2^k U_k with U_k
-// the sum of the S_b whose digit magnitude d = b + 1 has bit k set -- eight buckets each for
-// k < 4 (a quad adds two, then two levels inside its 16-lane row), U_4 = S_15 -- so the window needs
-// 3 quad additions after the bucket chains where k_batch_windows_q's scan + tree needs 8 (and its
-// unrolled straight-line code, fetched once per wave, cost 285 us for create_proof's two 64-term
-// MSMs at one wave per CU).  The host places U_k at exponent 5 w + k of one Horner.
+// Window sums for a host Horner (round 5, msm_batch_windows_host): one 256-thread block per (MSM,
+// window), 16 lanes per bucket.  Lane l of bucket b sums every 16th entry of the bucket (from the
+// l-th) with mixed additions: a chain of at most ceil(n_b / 16) -- the top window of a 128-bit GLV
+// half holds 2-3 bits, so its entries crowd into 3-4 buckets, and with 4 lanes per bucket its
+// chain of ~10 additions set the kernel time (149 us for create_proof's two 64-term MSMs).  The 16
+// partial sums of a bucket go to quad form (4 quads) and add in two levels; then
+// sum_b (b + 1) S_b = sum_k 2^k U_k with U_k the sum of the S_b whose digit magnitude d = b + 1 has
+// bit k set -- eight buckets each for k < 4 (a quad adds two, then two levels inside its 16-lane
+// row), U_4 = S_15 -- on wave 0.  Every quad addition runs through ONE call site (a loop over the
+// steps), so the code a wave fetches stays small.  The host places U_k at exponent 5 w + k of one
+// Horner.
 constexpr int kUPerWin = kQC;  // U_0 .. U_4
-__global__ void __launch_bounds__(64) k_batch_uwin(const uint64_t* __restrict__ off, uint32_t max_terms,
-                                                   const uint8_t* __restrict__ dig, const G1Aff* __restrict__ pts,
-                                                   G1Xyzz* __restrict__ U) {
+constexpr int kUwThreads = 256, kUL = kUwThreads / kQB;  // 16 lanes per bucket
+__global__ void __launch_bounds__(kUwThreads) k_batch_uwin(const uint64_t* __restrict__ off, uint32_t max_terms,
+                                                           const uint8_t* __restrict__ dig, const G1Aff* __restrict__ pts,
+                                                           G1Xyzz* __restrict__ U) {
   __shared__ BucketSmem sm;
   __shared__ Fq sb[kQB][4];
-  const uint32_t k = blockIdx.x, w = blockIdx.y;
-  const int c = threadIdx.x & 3, b = threadIdx.x >> 2;
-  const Fq S = bucket_sum_q(sm, k, w, off, nullptr, max_terms, dig, pts);
-  sb[b][c] = S;
+  const uint32_t k = blockIdx.x, w = blockIdx.y, t = threadIdx.x;
+  const uint32_t m = (uint32_t)(off[k + 1] - off[k]);
+  const uint8_t* dg = dig + ((size_t)k * kQW + w) * 2 * (size_t)max_terms;
+  // LDS counting sort of the window's 2m digits by bucket
+  if (t < kQB) sm.cnt[t] = 0;
   __syncthreads();
-  const int kk = b >> 2, j = b & 3;  // quad (kk, j): members j and j + 4 of U_kk
-  auto member = [&](int i) {         // the i-th magnitude with bit kk set, as its bucket index
+  for (uint32_t j = t; j < 2 * m; j += kUwThreads) {
+    const uint32_t d = dg[j];
+    if (d & 0x7f) atomicAdd(&sm.cnt[(d & 0x7f) - 1], 1u);
+  }
+  __syncthreads();
+  if (t == 0) {
+    uint32_t a = 0;
+    for (int bb = 0; bb < kQB; bb++) {
+      sm.start[bb] = a;
+      a += sm.cnt[bb];
+      sm.cnt[bb] = sm.start[bb];
+    }
+    sm.start[kQB] = a;
+  }
+  __syncthreads();
+  for (uint32_t j = t; j < 2 * m; j += kUwThreads) {
+    const uint32_t d = dg[j];
+    if (d & 0x7f) sm.lst[atomicAdd(&sm.cnt[(d & 0x7f) - 1], 1u)] = (uint16_t)(j | ((d >> 7) << 15));
+  }
+  __syncthreads();
+  const int b = t / kUL, l = t % kUL, c = t & 3;
+  const G1Aff* pk = pts + 2 * (size_t)k * max_terms;
+  G1Xyzz acc = G1Xyzz::identity();
+  for (uint32_t e = sm.start[b] + l; e < sm.start[b + 1]; e += kUL) {
+    const uint32_t v = sm.lst[e];
+    const uint32_t* pp = reinterpret_cast<const uint32_t*>(pk + (v & 0x7fff));
+    const Fq x = ld_fq(pp);
+    Fq y = ld_fq(pp + 8);
+    if (x.is_zero() && y.is_zero()) continue;  // identity base
+    if (v >> 15) y = -y;
+    acc = xyzz_madd_2p(acc, x, y);
+  }
+  Fq q[4] = {acc.X, acc.Y, acc.ZZ, acc.ZZZ};
+  quad::transpose(q, c);  // lane c: coordinate c of the quad's four partial sums
+  // steps 0-2: a quad's four sums; 3, 4: + quad qb + 2 (qb < 2), + quad qb + 1 (qb = 0) inside the
+  // bucket's 16 lanes; then S_b through LDS; 5: U_kk's members j, j + 4; 6, 7: two levels inside
+  // the 16-lane row (wave 0 only from step 5 on)
+  const int qb = l >> 2;                           // quad of the bucket
+  const int kk = (t >> 2) >> 2, j = (t >> 2) & 3;  // wave 0, quad (kk, j): members j and j + 4 of U_kk
+  auto member = [&](int i) {                       // the i-th magnitude with bit kk set, as its bucket index
     return ((((i >> kk) << (kk + 1)) | (1 << kk) | (i & ((1 << kk) - 1))) - 1);
   };
-  Fq u = quad::add_2p(sb[member(j)][c], sb[member(j + 4)][c], c);
-  Fq o = quad::down(u, 8);  // (every shuffle runs on every lane; the additions are quad-uniform)
-  if (j < 2) u = quad::add_2p(u, o, c);
-  o = quad::down(u, 4);
-  if (j == 0) u = quad::add_2p(u, o, c);
+  Fq x = q[0], S15 = q[0];
+#pragma unroll 1
+  for (int step = 0; step < 8; step++) {
+    Fq y;
+    if (step < 3) {
+      y = quad::pick(step == 0, q[1], quad::pick(step == 1, q[2], q[3]));
+    } else if (step < 5) {
+      y = quad::down(x, step == 3 ? 8 : 4);  // every shuffle runs on every lane
+    } else if (step == 5) {
+      if (qb == 0) sb[b][c] = x;  // S_b
+      __syncthreads();
+      if (t >= 64) break;  // wave-uniform: the U stage runs on wave 0
+      S15 = sb[kQB - 1][c];
+      x = sb[member(j)][c];
+      y = sb[member(j + 4)][c];
+    } else {
+      y = quad::down(x, step == 6 ? 8 : 4);
+    }
+    const Fq r = quad::add_2p(x, y, c);
+    const bool take = step < 3 || (step == 3 && qb < 2) || (step == 4 && qb == 0) || step == 5 ||
+                      (step == 6 && j < 2) || (step == 7 && j == 0);  // quad-uniform
+    x = quad::pick(take, r, x);
+  }
+  if (t >= 64) return;
   G1Xyzz* dst = U + ((size_t)k * kQW + w) * kUPerWin;
-  if (j == 0) quad::st(dst + kk, c, fe_canon2p(u));
-  if (b == kQB - 1) quad::st(dst + 4, c, fe_canon2p(S));  // U_4 = S_15 (magnitude 16)
+  if (j == 0) quad::st(dst + kk, c, fe_canon2p(x));
+  if (t < 4) quad::st(dst + 4, c, fe_canon2p(S15));  // U_4 = S_15 (magnitude 16)
 }
 
 // Bounded wait for a window's bucket sums (fused kernel): a wave that never sees the flag (a bug,
@@ -1142,7 +1215,7 @@ int msm_batch_windows_host(const void* d_bases, const void* d_scalars, const uin
                      dim3(kThreads), 0, st, static_cast<const G1Aff*>(d_bases), static_cast<const Fr*>(d_scalars),
                      d_offsets, nullptr, scalar_form == SV_MONTGOMERY ? 1 : 0, (uint32_t)max_terms, dig, pts, err,
                      nullptr, (uint64_t)0, base_form == SV_MONTGOMERY ? 1 : 0);
-  hipLaunchKernelGGL(k_batch_uwin, dim3((uint32_t)count, (uint32_t)kQW), dim3(64), 0, st, d_offsets,
+  hipLaunchKernelGGL(k_batch_uwin, dim3((uint32_t)count, (uint32_t)kQW), dim3(kUwThreads), 0, st, d_offsets,
                      (uint32_t)max_terms, dig, pts, Tg);
   SV_HIP(hipGetLastError());
   SV_HIP(hipMemcpyAsync(ws->pinned, blk, back, hipMemcpyDeviceToHost, st));

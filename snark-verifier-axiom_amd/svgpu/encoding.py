@@ -16,6 +16,7 @@ from . import _lib
 P = 21888242871839275222246405745257275088696311157297823662689037894645226208583
 R = 21888242871839275222246405745257275088548364400416034343698204186575808495617
 _MASK256 = (1 << 256) - 1
+_ZERO64 = bytes(64)
 
 
 def _to_form(x: int, mod: int, form: int) -> int:
@@ -45,6 +46,10 @@ def scalars_array(scalars: Sequence[int], form: int = _lib.SV_CANONICAL) -> np.n
 
 
 def bases_array(points: Sequence[Optional[Tuple[int, int]]], form: int = _lib.SV_CANONICAL) -> np.ndarray:
+    if form == _lib.SV_CANONICAL:  # one bytes join (2x faster than the generic path: config 5's encode)
+        buf = b"".join(_ZERO64 if pt is None else (pt[0] % P).to_bytes(32, "little") + (pt[1] % P).to_bytes(32, "little")
+                       for pt in points)
+        return np.frombuffer(buf, dtype=np.uint64).reshape(len(points), 8).copy()
     flat: List[int] = []
     for pt in points:
         if pt is None:

@@ -769,6 +769,7 @@ __device__ __forceinline__ Lz lane_sum(const Lz& re, const Lz& im) {
   return v;
 }
 
+// (the 9-limb carry form above is the round-4 lane sum, kept for tools/ubench_wg.hip's op A/B)
 // a lane's contribution l (a reduced v, doubled or not) placed in a coefficient: a real-part term
 // (l, 0) or an imaginary one (0, l); wrapped terms (index sum >= 6) carry xi = 9 + u:
 // (l, 0) -> (9l, l), (0, l) -> (-l, 9l) with -l from the negated reduced value nv
@@ -783,6 +784,122 @@ __device__ __forceinline__ void place(const Lz& l, const Lz& nl, bool imag, bool
   }
 }
 
+// ---- Round 5: lane sums in 24-bit signed limbs.  A lane's contribution to its coefficient's
+// (re, im) is (m_re v, m_im v) for its product v in [0, 2p) and small signed integers fixed by the
+// lane's role (the sign of a1 b1 in the real part, the 2 of a cross term, the xi = 9 + u wrap, 0
+// for an idle lane: WLane), so the placement is a multiply per limb instead of negations, doublings
+// and selects.  v splits into 11 limbs of 24 bits (one v_perm_b32 each).  Over one coefficient the
+// |m| sum to at most 102 (positive ones to 97, negative ones to 56, w_mul and w_sqr alike), and
+// 102 * 2^24 < 2^31, so every partial sum stays an int32 per limb and a level of the lane sum is
+// ONE v_add_u32 per limb with the partner's limb read through DPP: no carry chain, whose VCC
+// hazards cost an s_nop per dependent v_addc.  The coefficient sum lies in (-112 p, 194 p);
+// biased by 240 p it is positive and below 434 p < 2^263, and one signed carry pass normalises it
+// into the 9-word Lz form that lz_reduce takes.
+constexpr int kL24 = 11;  // 11 x 24 = 264 bits
+struct Limbs24 {
+  uint32_t v[kL24];
+};
+constexpr Limbs24 make_bias24() {  // 240 p in 24-bit limbs
+  uint32_t w[9] = {};
+  uint64_t c = 0;
+  for (int i = 0; i < 8; i++) {
+    const uint64_t x = (uint64_t)FQ_P[i] * 240u + c;
+    w[i] = (uint32_t)x;
+    c = x >> 32;
+  }
+  w[8] = (uint32_t)c;
+  Limbs24 b{};
+  for (int i = 0; i < kL24; i++) {
+    const int wi = 24 * i / 32, o = 24 * i % 32;
+    const uint64_t x = (uint64_t)w[wi] | (wi + 1 < 9 ? (uint64_t)w[wi + 1] << 32 : 0);
+    b.v[i] = (uint32_t)(x >> o) & 0xFFFFFFu;
+  }
+  return b;
+}
+constexpr Limbs24 kBias24 = make_bias24();
+static_assert(kBias24.v[kL24 - 1] < (1u << 22), "240 p < 2^262");
+// byte B of a 256-bit value is byte B % 4 of word B / 4; limb i = bytes 3i .. 3i + 2
+__device__ __forceinline__ void split24(const Fq& a, uint32_t l[kL24]) {
+#pragma unroll
+  for (int i = 0; i < kL24; i++) {
+    const int w = 3 * i / 4, o = 3 * i % 4;
+    const uint32_t lo = a.v[w], hi = w + 1 < 8 ? a.v[w + 1] : 0u;
+    // selector bytes 0-3 pick from lo, 4-7 from hi, 0x0C gives zero
+    const uint32_t sel = (uint32_t)o | (uint32_t)(o + 1) << 8 | (uint32_t)(o + 2) << 16 | 0x0C000000u;
+    l[i] = __builtin_amdgcn_perm(hi, lo, sel);
+  }
+}
+// biased signed-limb sum -> 9 words: carries t_i >> 24 (arithmetic); word j = bytes 4j .. 4j + 3
+// gathered from the low three bytes of two adjacent t (v_perm_b32); the top word takes all of t_10
+// above bit 16 (the biased sum is non-negative)
+__device__ __forceinline__ Lz norm24(const uint32_t s[kL24]) {
+  uint32_t t[kL24];
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < kL24; i++) {
+    t[i] = s[i] + kBias24.v[i] + (uint32_t)c;
+    c = (int32_t)t[i] >> 24;
+  }
+  Lz r;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int l0 = 4 * j / 3;
+    uint32_t sel = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int B = 4 * j + k, li = B / 3, pos = B % 3;
+      sel |= (uint32_t)(li == l0 ? pos : 4 + pos) << (8 * k);
+    }
+    r.v[j] = __builtin_amdgcn_perm(t[l0 + 1], t[l0], sel);
+  }
+  r.v[8] = t[kL24 - 1] >> 16;
+  return r;
+}
+// the coefficient sum of m_keep v over the lanes of an aligned group of 2^LEVELS lanes, as the
+// reduce-scatter of lane_sum: level 1 adds the neighbour's m_send v, so even lanes carry re and odd
+// lanes im; later levels pair lanes of equal parity (lane ^ 2, row rotations by 4 and 8, lane ^ 16)
+// x + (x of the partner lane L): the move written as update_dpp with a zero "old" and bound_ctrl
+// so the compiler folds it into the add (v_add_u32_dpp); the swizzle level stays a move + add
+template <int L>
+__device__ __forceinline__ uint32_t add_x(uint32_t acc, uint32_t x) {
+  constexpr int ctrl = L == 0 ? 0xB1 : L == 1 ? 0x4E : L == 5 ? 0x124 : L == 6 ? 0x128 : -1;
+  if constexpr (ctrl < 0) return acc + xmove<L>(x);
+  else return acc + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, ctrl, 0xF, 0xF, true);
+}
+template <int LEVELS>
+__device__ __forceinline__ Lz lane_sum24(const Fq& v, uint32_t m_keep, uint32_t m_send) {
+  static_assert(LEVELS == 2 || LEVELS == 4 || LEVELS == 5, "row rotations need 16-lane groups");
+  uint32_t l[kL24], x[kL24];
+  split24(v, l);
+#pragma unroll
+  for (int i = 0; i < kL24; i++) x[i] = add_x<0>(m_keep * l[i], m_send * l[i]);
+#pragma unroll
+  for (int i = 0; i < kL24; i++) x[i] = add_x<1>(x[i], x[i]);
+  if constexpr (LEVELS > 2) {
+#pragma unroll
+    for (int i = 0; i < kL24; i++) x[i] = add_x<5>(x[i], x[i]);
+#pragma unroll
+    for (int i = 0; i < kL24; i++) x[i] = add_x<6>(x[i], x[i]);
+  }
+  if constexpr (LEVELS > 4) {
+#pragma unroll
+    for (int i = 0; i < kL24; i++) x[i] = add_x<4>(x[i], x[i]);
+  }
+  return norm24(x);
+}
+// a lane's (keep, send) multipliers from its (re, im) ones: the xi wrap (r, i) -> (9r - i, r + 9i),
+// even lanes keep re, odd lanes im
+__device__ __forceinline__ void keep_send(int re, int im, bool wrap, uint32_t& keep, uint32_t& send) {
+  if (wrap) {
+    const int r = 9 * re - im, i = re + 9 * im;
+    re = r;
+    im = i;
+  }
+  const bool odd = threadIdx.x & 1;
+  keep = (uint32_t)(odd ? im : re);
+  send = (uint32_t)(odd ? re : im);
+}
+
 // Per-lane roles of w_mul / w_sqr, fixed for the whole program (computed once, kept in registers:
 // the square-term table lookup was a per-operation vector load on the critical path).
 struct WLane {
@@ -792,6 +909,8 @@ struct WLane {
   // w_sqr: coefficient, pair {si, sj}, partial product q, flags
   uint8_t sk, si, sj, sq;
   bool slive, ssquare, sxi, sgrp;
+  // lane_sum24 multipliers of w_mul, w_sqr and w_frob (frob: for even n; odd n negates odd q)
+  uint32_t mkeep, msend, skeep, ssend, fkeep, fsend;
 };
 __device__ __forceinline__ WLane wlane_init() {
   WLane L{};
@@ -818,6 +937,23 @@ __device__ __forceinline__ WLane wlane_init() {
     L.ssquare = L.si == L.sj;
     L.sxi = L.slive && tm.xi;
   }
+  {  // w_mul q: 0 a0 b0 (re +), 1 a1 b1 (re -), 2 a0 b1 (im), 3 a1 b0 (im)
+    const int q = L.mq;
+    const int re = !L.mact ? 0 : (q == 0 ? 1 : (q == 1 ? -1 : 0)), im = L.mact && q >= 2 ? 1 : 0;
+    keep_send(re, im, L.mwrap, L.mkeep, L.msend);
+  }
+  {  // w_sqr q: a square a0^2 (re +), a1^2 (re -), 2 a0 a1 (im); a cross term twice the w_mul terms
+    const int q = L.sq, f = L.ssquare ? 1 : 2;
+    int re = q == 0 ? f : (q == 1 ? -f : 0), im = q == 2 ? 2 : (q == 3 && !L.ssquare ? 2 : 0);
+    if (!L.slive) re = im = 0;
+    keep_send(re, im, L.sxi, L.skeep, L.ssend);
+  }
+  {  // w_frob lanes t < 24: coefficient t >> 2, q = t & 3 as in w_mul
+    const int q = t & 3;
+    const bool act = (t >> 2) < 6;
+    const int re = !act ? 0 : (q == 0 ? 1 : (q == 1 ? -1 : 0)), im = act && q >= 2 ? 1 : 0;
+    keep_send(re, im, false, L.fkeep, L.fsend);
+  }
   return L;
 }
 
@@ -831,15 +967,11 @@ SV_WG_FN void w_mul(const WLane& L, Fq2* __restrict__ dst, const Fq2* a, const F
   const int t = threadIdx.x;
   if (t < 192) {  // waves 0-2 (uniform per wave)
     const int q = L.mq;
-    // q: 0 a0 b0 (re +), 1 a1 b1 (re -), 2 a0 b1 (im +), 3 a1 b0 (im +)
+    // q: 0 a0 b0 (re +), 1 a1 b1 (re -), 2 a0 b1 (im +), 3 a1 b0 (im +); idle lanes multiply by 0
     const Fq ax = ld_fq((q & 1) ? &a[L.mi].c1 : &a[L.mi].c0);
     const Fq by = ld_fq((q == 1 || q == 2) ? &b[L.mjj].c1 : &b[L.mjj].c0);
-    Fq v = fe_mul_lazy(ax, by);  // [0, 2p): the lane sums reduce once per coefficient
-    if (!L.mact) v = Fq::zero();
-    const Fq nv = fq_neg2p(v);
-    Lz re, im;
-    place(lz(q == 1 ? nv : v), lz(q == 1 ? v : nv), q >= 2, L.mwrap, re, im);
-    store_coeff(dst, L.mk, t & 31, lane_sum<5>(re, im));
+    // [0, 2p): the lane sums reduce once per coefficient
+    store_coeff(dst, L.mk, t & 31, lane_sum24<5>(fe_mul_lazy(ax, by), L.mkeep, L.msend));
   }
   __syncthreads();
 }
@@ -855,42 +987,25 @@ SV_WG_FN void w_sqr(const WLane& L, Fq2* __restrict__ dst, const Fq2* a) {
     // takes x from a_i (q odd: c1) and y from a_j (q 1, 2: c1)
     const bool xc1 = square ? q == 1 : (q & 1);
     const bool yc1 = square ? q != 0 : (q == 1 || q == 2);
-    const bool imag = square ? q == 2 : q >= 2;
     const Fq x = ld_fq(xc1 ? &a[L.si].c1 : &a[L.si].c0);
     const Fq y = ld_fq(yc1 ? &a[L.sj].c1 : &a[L.sj].c0);
-    Fq v = fe_mul_lazy(x, y);
-    if (!L.slive || (square && q == 3)) v = Fq::zero();
-    const Fq nv = fq_neg2p(v);
-    const bool neg = q == 1;
-    Lz l = lz(neg ? nv : v), nl = lz(neg ? v : nv);
-    if (!square || q == 2) {  // the pair counted twice / the 2 a0 a1 of a square
-      l = lz_add(l, l);
-      nl = lz_add(nl, nl);
-    }
-    Lz re, im;
-    place(l, nl, imag, L.sxi, re, im);
-    const Lz s = lane_sum<4>(re, im);
+    const Lz s = lane_sum24<4>(fe_mul_lazy(x, y), L.skeep, L.ssend);
     if (L.sgrp) store_coeff(dst, L.sk, t & 15, s);
   }
   __syncthreads();
 }
 
 // dst = frob^n(a): coefficient k -> conj^n(a_k) * gamma_(n,k); gam = c_gamma staged in LDS
-SV_WG_FN void w_frob(Fq2* __restrict__ dst, const Fq2* a, int n, const Fq* gam) {
+SV_WG_FN void w_frob(const WLane& L, Fq2* __restrict__ dst, const Fq2* a, int n, const Fq* gam) {
   const int t = threadIdx.x;
   if (t < 64) {
     const int k = t >> 2, q = t & 3;
     const bool act = k < 6;
     const int kk = act ? k : 0;
-    Fq x = ld_fq((q & 1) ? &a[kk].c1 : &a[kk].c0);
-    if ((n & 1) && (q & 1)) x = fq_neg2p(x);
+    const Fq x = ld_fq((q & 1) ? &a[kk].c1 : &a[kk].c0);
     const Fq gc = ld_fq(gam + ((n - 1) * 6 + kk) * 2 + ((q == 1 || q == 2) ? 1 : 0));
-    Fq v = fe_mul_lazy(x, gc);
-    if (!act) v = Fq::zero();
-    const Fq nv = fq_neg2p(v);
-    Lz re, im;
-    place(lz(q == 1 ? nv : v), lz(q == 1 ? v : nv), q >= 2, false, re, im);
-    const Lz s = lane_sum<2>(re, im);
+    const bool flip = (n & 1) && (q & 1);  // conj^n: odd n negates a_k's c1 (the odd q lanes' x)
+    const Lz s = lane_sum24<2>(fe_mul_lazy(x, gc), flip ? 0u - L.fkeep : L.fkeep, flip ? 0u - L.fsend : L.fsend);
     if (act) store_coeff(dst, k, q, s);
   }
   __syncthreads();
@@ -1182,7 +1297,7 @@ __global__ void __launch_bounds__(wg::kThreads) k_decide_wg(const G1Aff* __restr
     switch (op.code) {
       case OP_MUL: w_mul(Ln, dst, a, opnd(op.b)); break;
       case OP_SQR: w_sqr(Ln, dst, a); break;
-      case OP_FROB: w_frob(dst, a, op.imm, gam); break;
+      case OP_FROB: w_frob(Ln, dst, a, op.imm, gam); break;
       case OP_CONJ: w_conj(dst, a, true); break;
       case OP_COPY: w_conj(dst, a, false); break;
       default: w_norm_inv(dst, a, tj, &di); break;

@@ -1,6 +1,7 @@
 """Static instruction counts of a gfx950 kernel's hot loop, from the compiler's assembly.
 
-python tools/isa_count.py [KERNEL_SUBSTRING]   (default: the 29-bit bucket chain k_accumulate<false, true, 1>)
+python tools/isa_count.py [KERNEL_SUBSTRING [SOURCE]]   (default: the 29-bit bucket chain
+k_accumulate<false, true, 1> of csrc/msm.hip; e.g. `k_decide_wg decider.hip` for the decider)
 
 Compiles snark-verifier-axiom_amd/csrc/msm.hip with hipcc -S (device only), takes the kernel's body,
 and splits it at its basic blocks.  The XYZZ mixed addition's common path (no segment end, no
@@ -18,7 +19,7 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "snark-verifier-axiom_amd", "csrc", "msm.hip")
+SRC = os.path.join(ROOT, "snark-verifier-axiom_amd", "csrc", sys.argv[2] if len(sys.argv) > 2 else "msm.hip")
 KEY = sys.argv[1] if len(sys.argv) > 1 else "k_accumulateILb0ELb1ELi1E"
 
 

@@ -1270,8 +1270,16 @@ __global__ void __launch_bounds__(wg::kThreads) k_decide_wg(const G1Aff* __restr
     pair_products(D, E, t, kThreads);
   }
   __syncthreads();
+#if defined(SV_WG_PROLOGUE_ONLY) && SV_WG_PROLOGUE_ONLY == 1
+  if (t == 0) verdict[acc] = 0;  // timing of the pair products alone
+  return;
+#endif
   merge_products(M, D, t, kThreads);  // (a divergence-free 5-term walk measured no faster)
   __syncthreads();
+#if defined(SV_WG_PROLOGUE_ONLY) && SV_WG_PROLOGUE_ONLY == 2
+  if (t == 0) verdict[acc] = 0;  // timing through the merged products
+  return;
+#endif
   Fq2* Y = M + 6 * kMaxMerge;  // the paired steps' products, behind M in the dead line region
   if (paired) {
     pair_steps(S, Y, D, M, t, kThreads);

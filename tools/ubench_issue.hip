@@ -88,6 +88,107 @@ __global__ void __launch_bounds__(256, 4) k_alt(uint64_t* out, int iters) {
   out[tid] = s;
 }
 
+// dependent-chain latency at ONE wave per SIMD (the decider's occupancy): C independent
+// v_mad_u64_u32 chains per iteration; cycles per iteration / C = the issue cost once C chains
+// cover the latency, cycles per iteration = the latency of one dependent mad while C = 1
+template <int C, int ADDC>
+__global__ void __launch_bounds__(64) k_lat(uint64_t* out, int iters, unsigned long long* cyc) {
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t acc[C];
+  uint32_t a[C], b[C], o[C];
+#pragma unroll
+  for (int j = 0; j < C; j++) {
+    acc[j] = tid + j;
+    a[j] = tid * 3 + j;
+    b[j] = tid ^ (j * 77);
+    o[j] = 0;
+  }
+  const unsigned long long t0 = clock64();
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int j = 0; j < C; j++) {
+      if constexpr (ADDC)
+        asm volatile("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
+                     : "+v"(acc[j]), "+v"(o[j]) : "v"(a[j]), "v"(b[j]) : "vcc");
+      else
+        asm volatile("v_mad_u64_u32 %0, s[0:1], %1, %2, %0" : "+v"(acc[j]) : "v"(a[j]), "v"(b[j]) : "s0", "s1");
+    }
+  }
+  const unsigned long long t1 = clock64();
+  uint64_t s = 0;
+#pragma unroll
+  for (int j = 0; j < C; j++) s += acc[j] + o[j];
+  out[tid] = s;
+  if (tid == 0) *cyc = t1 - t0;
+}
+template <int C, int ADDC>
+static void lat(const char* name, uint64_t* d, unsigned long long* dc) {
+  const int iters = 4096;
+  hipLaunchKernelGGL((k_lat<C, ADDC>), dim3(1), dim3(64), 0, 0, d, 16, dc);
+  hipLaunchKernelGGL((k_lat<C, ADDC>), dim3(1), dim3(64), 0, 0, d, iters, dc);
+  unsigned long long c = 0;
+  (void)hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
+  printf("one wave, %-24s %2d chain(s): %6.2f cycles per iteration, %5.2f per instruction group\n", name, C,
+         (double)c / iters, (double)c / iters / C);
+}
+
+// single-wave issue interval of one instruction type: 8 independent chains per iteration, 16
+// iterations unrolled per loop trip (loop overhead / 128), one block of T threads (T = 64: one wave
+// on one SIMD; T = 512: two waves per SIMD)
+// OP: 0 v_mad_u64_u32, 1 v_add_u32, 2 v_add_co_u32 + v_addc_co_u32 (one pair), 3 v_mul_lo_u32,
+//     4 v_perm_b32, 5 v_add_u32_dpp (row_ror:4), 6 v_mov_b32_dpp + v_add_u32 (pair)
+template <int OP>
+__global__ void __launch_bounds__(512) k_one(uint64_t* out, int iters, unsigned long long* cyc) {
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t acc[8];
+  uint32_t a[8], b[8], x[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    acc[j] = tid + j;
+    a[j] = tid * 3 + j;
+    b[j] = tid ^ (j * 77);
+    x[j] = tid * 7 + j;
+  }
+  const unsigned long long t0 = clock64();
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        if constexpr (OP == 0) asm volatile("v_mad_u64_u32 %0, s[0:1], %1, %2, %0" : "+v"(acc[j]) : "v"(a[j]), "v"(b[j]) : "s0", "s1");
+        if constexpr (OP == 1) asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[j]) : "v"(a[j]));
+        if constexpr (OP == 2)
+          asm volatile("v_add_co_u32 %0, vcc, %0, %2\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
+                       : "+v"(x[j]), "+v"(a[j]) : "v"(b[j]) : "vcc");
+        if constexpr (OP == 3) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x[j]) : "v"(b[j]));
+        if constexpr (OP == 4) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(x[j]) : "v"(b[j]), "v"(a[j]));
+        if constexpr (OP == 5) asm volatile("v_add_u32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf bound_ctrl:0" : "+v"(x[j]));
+        if constexpr (OP == 6)
+          asm volatile("v_mov_b32_dpp %1, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\ts_nop 1\n\tv_add_u32 %0, %0, %1"
+                       : "+v"(x[j]), "+v"(a[j]));
+      }
+    }
+  }
+  const unsigned long long t1 = clock64();
+  uint64_t s = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) s += acc[j] + x[j] + a[j];
+  out[tid] = s;
+  if (threadIdx.x == 0) *cyc = t1 - t0;
+}
+template <int OP>
+static void one(const char* name, uint64_t* d, unsigned long long* dc) {
+  const int iters = 256;
+  for (int T : {64, 512}) {
+    hipLaunchKernelGGL(k_one<OP>, dim3(1), dim3(T), 0, 0, d, 4, dc);
+    hipLaunchKernelGGL(k_one<OP>, dim3(1), dim3(T), 0, 0, d, iters, dc);
+    unsigned long long c = 0;
+    (void)hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
+    printf("%-28s %s: %6.2f cycles per instruction (group) per wave\n", name,
+           T == 64 ? "1 wave / SIMD " : "2 waves / SIMD", (double)c / (iters * 128.0));
+  }
+}
+
 template <typename K>
 static float run(const char* name, K kern, uint64_t* d, double others_per_mad, float base) {
   hipEvent_t e0, e1;
@@ -133,5 +234,21 @@ int main() {
   run("add_u32 only (as mads)", k_alt<0>, (uint64_t*)d, 0, 0);
   const float m16 = run("16 mad chains (x2)", k_alt<1>, (uint64_t*)d, 0, 0);
   printf("16 mad chains: %.2f cycles per mad\n", m16 * 1e-3 * 2.4e9 * 1024 / (8192.0 * 256 / 64 * 1000 * 16));
+  unsigned long long* dc;
+  CK(hipMalloc(&dc, 8));
+  lat<1, 0>("mad", (uint64_t*)d, dc);
+  lat<2, 0>("mad", (uint64_t*)d, dc);
+  lat<4, 0>("mad", (uint64_t*)d, dc);
+  lat<8, 0>("mad", (uint64_t*)d, dc);
+  lat<1, 1>("mad + addc (vcc)", (uint64_t*)d, dc);
+  lat<2, 1>("mad + addc (vcc)", (uint64_t*)d, dc);
+  lat<4, 1>("mad + addc (vcc)", (uint64_t*)d, dc);
+  one<0>("v_mad_u64_u32", (uint64_t*)d, dc);
+  one<1>("v_add_u32", (uint64_t*)d, dc);
+  one<2>("v_add_co + v_addc (pair)", (uint64_t*)d, dc);
+  one<3>("v_mul_lo_u32", (uint64_t*)d, dc);
+  one<4>("v_perm_b32", (uint64_t*)d, dc);
+  one<5>("v_add_u32_dpp row_ror", (uint64_t*)d, dc);
+  one<6>("v_mov_dpp + v_add (pair)", (uint64_t*)d, dc);
   return 0;
 }

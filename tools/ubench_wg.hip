@@ -29,7 +29,7 @@ __global__ void __launch_bounds__(256) k_bench(int op, int iters, unsigned long 
   for (int i = 0; i < iters; i++) {
     if (op == 0) wg::w_sqr(L, c, a);
     else if (op == 1) wg::w_mul(L, c, a, b);
-    else if (op == 2) wg::w_frob(c, a, 1, gam);
+    else if (op == 2) wg::w_frob(L, c, a, 1, gam);
     else wg::w_conj(c, a);
     Fq2* tmp = a;
     a = c;

@@ -613,10 +613,12 @@ __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ l
 }
 
 // =============================================================================================
-// Workgroup decider (default): one 256-thread block -- four waves, one per SIMD of a CU -- per
-// accumulator.  The single-wave kernel above keeps one SIMD busy per accumulator, so 256
-// accumulators leave three quarters of the chip's 1024 SIMDs idle, and each of its lanes runs two or
-// three dependent Fq products per Fq12 operation (~0.65 us each on one wave).  Here every Fq12
+// Workgroup decider (default): one block per accumulator -- 512 threads since round 5, two waves per
+// SIMD of a CU (the Fq12 operations below use waves 0-2; the prologue's independent jobs use all
+// eight, and a second wave on a SIMD issues at the full single-wave rate: tools/ubench_issue.hip).
+// The single-wave kernel above keeps one SIMD busy per accumulator, so 256 accumulators leave three
+// quarters of the chip's 1024 SIMDs idle, and each of its lanes runs two or three dependent Fq
+// products per Fq12 operation (~0.65 us each on one wave).  Here every Fq12
 // operation spreads its Fq products over the block, ONE product per lane:
 //   w_mul   144 lanes (6 output coefficients x 6 terms x 4 schoolbook Fq2 partial products),
 //   w_sqr    96 lanes (6 coefficients x <= 4 pair terms x <= 4 partial products),
@@ -633,7 +635,10 @@ __global__ void __launch_bounds__(64) k_decide_lanes(const G1Aff* __restrict__ l
 #define SV_WG_FN __device__ __forceinline__
 #endif
 namespace wg {
-constexpr int kThreads = 256;
+#ifndef SV_WG_THREADS
+#define SV_WG_THREADS 512
+#endif
+constexpr int kThreads = SV_WG_THREADS;  // two waves per SIMD: the prologue jobs run at twice the issue rate
 
 template <int L>
 __device__ __forceinline__ uint32_t xmove(uint32_t x) {
@@ -1232,11 +1237,77 @@ __device__ __forceinline__ void pair_steps(Fq2* __restrict__ Q, Fq2* __restrict_
   }
 }
 
+// ---- Round 5: the prologue's products one Fq2 product per lane job.  merge_products and
+// pair_steps above give each lane a whole output coefficient: 5-10 (merges) and 2 x 6 (paired
+// steps) dependent Fq2 products per lane, 23 + 48 us of the kernel with most of the block's
+// issue capacity unused (measured by SV_WG_PROLOGUE_ONLY builds).  Here every term product is its
+// own job (written to an LDS scratch X, with the w^6 = xi wrap applied), and after a barrier one
+// lane per output coefficient adds its terms: 575 + 744 + 1116 jobs over 256 lanes, 3 + 3 + 5
+// products deep instead of 10 + 12.  The values are the same canonical field elements.
+constexpr int kScratchJobs = kStepPairs * 36;  // the largest phase (Y_p = Q_p X_{j+1})
+static_assert(kMaxMerge * 25 <= kScratchJobs && kStepPairs * 24 <= kScratchJobs, "scratch holds every phase");
+// M_m = D_a D_{a+1} (both 5-sparse: coefficients 0-4) for every merged step
+__device__ __forceinline__ void merge_products_wide(Fq2* __restrict__ M, const Fq2* __restrict__ D, Fq2* __restrict__ X,
+                                                    int t, int nt) {
+  const int nm = c_merge.n;
+  for (int job = t; job < nm * 25; job += nt) {
+    const int m = job / 25, r = job % 25, i = r / 5, j = r % 5;
+    const Fq2* a = D + 6 * c_merge.first[m];
+    const Fq2 v = a[i] * a[6 + j];
+    X[job] = i + j >= 6 ? fq2_mul_xi(v) : v;
+  }
+  __syncthreads();
+  for (int job = t; job < nm * 6; job += nt) {
+    const int m = job / 6, k = job % 6;
+    Fq2 acc = Fq2::zero();
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const int j = k - i < 0 ? k - i + 6 : k - i;
+      if (j < 5) acc = acc + X[25 * m + 5 * i + j];
+    }
+    M[6 * m + k] = acc;
+  }
+}
+// Y_p = X_j^2 X_{j+1} (j = 1 + 2p): the square by c_sqr's pair terms (<= 4 per coefficient, cross
+// terms doubled), into Q (the slot region, free during the prologue), then the product's 36 terms
+__device__ __forceinline__ void pair_steps_wide(Fq2* __restrict__ Q, Fq2* __restrict__ Y, const Fq2* D, const Fq2* M,
+                                                Fq2* __restrict__ X, int t, int nt) {
+  for (int job = t; job < kStepPairs * 24; job += nt) {
+    const int pk = job >> 2, p = pk / 6, k = pk % 6;
+    const SqrTerm tm = c_sqr[k][job & 3];
+    const Fq2* x = step_x(c_steps.x[1 + 2 * p], D, M);
+    const bool live = tm.i >= 0;
+    Fq2 v = x[live ? tm.i : 0] * x[live ? tm.j : 0];
+    if (tm.dbl) v = v + v;
+    if (tm.xi) v = fq2_mul_xi(v);
+    X[job] = live ? v : Fq2::zero();
+  }
+  __syncthreads();
+  for (int job = t; job < kStepPairs * 6; job += nt)
+    Q[job] = (X[4 * job] + X[4 * job + 1]) + (X[4 * job + 2] + X[4 * job + 3]);
+  __syncthreads();
+  for (int job = t; job < kStepPairs * 36; job += nt) {
+    const int p = job / 36, r = job % 36, i = r / 6, j = r % 6;
+    const Fq2 v = Q[6 * p + i] * step_x(c_steps.x[2 + 2 * p], D, M)[j];
+    X[job] = i + j >= 6 ? fq2_mul_xi(v) : v;
+  }
+  __syncthreads();
+  for (int job = t; job < kStepPairs * 6; job += nt) {
+    const int p = job / 6, k = job % 6;
+    Fq2 acc = Fq2::zero();
+#pragma unroll
+    for (int i = 0; i < 6; i++) acc = acc + X[36 * p + 6 * i + (k - i < 0 ? k - i + 6 : k - i)];
+    Y[job] = acc;
+  }
+}
+
 constexpr size_t kLdsE = 2 * (size_t)ATE_NUM_LINES * sizeof(LineCoeff);
 constexpr size_t kLdsD = (size_t)ATE_NUM_LINES * 6 * sizeof(Fq2);
 constexpr size_t kLdsSlots = (size_t)kSlots * 6 * sizeof(Fq2);
 constexpr size_t kLdsGamma = sizeof(c_gamma);
-constexpr size_t kLds = kLdsE + kLdsD + kLdsSlots + kLdsGamma;
+constexpr size_t kLdsScratch = (size_t)kScratchJobs * sizeof(Fq2);
+constexpr size_t kLds = kLdsE + kLdsD + kLdsSlots + kLdsGamma + kLdsScratch;
+static_assert(kLds + 512 <= 160 * 1024, "the block's LDS (dynamic + static) fits a CU's 160 KiB");
 static_assert((size_t)(kMaxMerge + kStepPairs) * 6 * sizeof(Fq2) <= kLdsE, "M and Y fit the line region");
 }  // namespace wg
 
@@ -1244,7 +1315,7 @@ __global__ void __launch_bounds__(wg::kThreads) k_decide_wg(const G1Aff* __restr
                                                           uint32_t n, const LineCoeff* __restrict__ L1,
                                                           const LineCoeff* __restrict__ L2, int mont_in,
                                                           int32_t* __restrict__ verdict, Fq12* __restrict__ gt,
-                                                          const Fq2* __restrict__ kc, int paired) {
+                                                          const Fq2* __restrict__ kc, int paired, int wide) {
   using namespace wg;
   extern __shared__ __attribute__((aligned(16))) unsigned char dec_lds[];
   __shared__ Fq2 tj[3], di;
@@ -1253,6 +1324,7 @@ __global__ void __launch_bounds__(wg::kThreads) k_decide_wg(const G1Aff* __restr
   Fq2* S = reinterpret_cast<Fq2*>(dec_lds + kLdsE + kLdsD);
   Fq2* M = reinterpret_cast<Fq2*>(E);  // the evaluated lines are dead once M is formed
   Fq* gam = reinterpret_cast<Fq*>(dec_lds + kLdsE + kLdsD + kLdsSlots);
+  Fq2* X = reinterpret_cast<Fq2*>(dec_lds + kLdsE + kLdsD + kLdsSlots + kLdsGamma);  // prologue scratch
   const int t = threadIdx.x;
   for (int i = t; i < (int)(kLdsGamma / 4); i += kThreads) reinterpret_cast<uint32_t*>(gam)[i] = c_gamma[i];
   const uint32_t acc = blockIdx.x;
@@ -1274,7 +1346,8 @@ __global__ void __launch_bounds__(wg::kThreads) k_decide_wg(const G1Aff* __restr
   if (t == 0) verdict[acc] = 0;  // timing of the pair products alone
   return;
 #endif
-  merge_products(M, D, t, kThreads);  // (a divergence-free 5-term walk measured no faster)
+  if (wide) merge_products_wide(M, D, X, t, kThreads);
+  else merge_products(M, D, t, kThreads);  // (a divergence-free 5-term walk measured no faster)
   __syncthreads();
 #if defined(SV_WG_PROLOGUE_ONLY) && SV_WG_PROLOGUE_ONLY == 2
   if (t == 0) verdict[acc] = 0;  // timing through the merged products
@@ -1282,7 +1355,8 @@ __global__ void __launch_bounds__(wg::kThreads) k_decide_wg(const G1Aff* __restr
 #endif
   Fq2* Y = M + 6 * kMaxMerge;  // the paired steps' products, behind M in the dead line region
   if (paired) {
-    pair_steps(S, Y, D, M, t, kThreads);
+    if (wide) pair_steps_wide(S, Y, D, M, X, t, kThreads);
+    else pair_steps(S, Y, D, M, t, kThreads);
     __syncthreads();
   }
   const WProg& prog = paired ? c_wprog2 : c_wprog;
@@ -1466,6 +1540,8 @@ int decide_run_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const vo
   static const int phases = getenv("SVGPU_DECIDER_PHASES") ? atoi(getenv("SVGPU_DECIDER_PHASES")) : 3;
   // k_decide_wg's two Miller steps per product (SVGPU_DECIDER_PAIR=0: one per step), read per call
   const bool pair_env = !getenv("SVGPU_DECIDER_PAIR") || atoi(getenv("SVGPU_DECIDER_PAIR")) != 0;
+  // the prologue's products one per lane job (SVGPU_DECIDER_WIDE=0: one output coefficient per lane)
+  const bool wide_env = !getenv("SVGPU_DECIDER_WIDE") || atoi(getenv("SVGPU_DECIDER_WIDE")) != 0;
   const G1Aff* dl = reinterpret_cast<const G1Aff*>(d_lhs);
   const G1Aff* dr = reinterpret_cast<const G1Aff*>(d_rhs);
   const int mont = form == SV_MONTGOMERY ? 1 : 0;
@@ -1478,7 +1554,7 @@ int decide_run_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const vo
   }
   if (lanes == 256)
     hipLaunchKernelGGL(k_decide_wg, dim3((unsigned)n), dim3(wg::kThreads), wg::kLds, st, dl, dr, (uint32_t)n, lines,
-                       L2, mont, d_verdict, d_gt, kc_env ? line_ref->d_kc : nullptr, pair_env ? 1 : 0);
+                       L2, mont, d_verdict, d_gt, kc_env ? line_ref->d_kc : nullptr, pair_env ? 1 : 0, wide_env ? 1 : 0);
   else if (lanes == 48)
     hipLaunchKernelGGL(k_decide_lanes<8>, dim3((unsigned)n), dim3(64), 0, st, dl, dr, (uint32_t)n, lines, L2, mont,
                        d_verdict, d_gt, phases);

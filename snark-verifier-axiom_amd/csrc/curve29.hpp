@@ -3,6 +3,9 @@
 // Bounds (field29.hpp's lazy contract), kept by every function here:
 //   state  X < 4p, Y < 2p, ZZ < 2p, ZZZ < 2p; the identity is exactly all-zero limbs (ZZ == 0: a
 //          non-identity state never has ZZ = 0 mod p, since ZZ3 = ZZ PP and PP != 0 mod p);
+//          madd's chain state (round 5) lets X reach 8p: its X3 skips the conditional subtraction,
+//          and whoever stores the chain's sum brings X below 4p (k_accumulate: csub<4> at a
+//          segment's end, AccChain<true>::out);
 //   point  x2, y2 below 2p (R' form), never the identity (callers skip it).
 // The formulas are madd-2008-s / mdbl-2008-s, as xyzz_madd_2p / xyzz_mdbl in curve.hpp.
 #pragma once
@@ -31,27 +34,33 @@ SV29_HD bool is_identity(const Xyzz& p) { return is_zero(p.ZZ); }
 // X3 = M^2 - 2S, Y3 = M (S - X3) - y2 W, ZZ3 = V, ZZZ3 = W its outputs with (X, Y, ZZ, ZZZ) =
 // (x2, y2, 1, 1) and no PPP term in X3 -- the rare branch only sets operands (one extra square),
 // so the chain holds no registers for a separate doubling (k_accumulate fits 128 VGPRs).
-SV29_HD Xyzz madd(const Xyzz& p, const F& x2, const F& y2) {
-  if (is_identity(p)) return {x2, y2, one(), one()};
-  F Pd = sub<4>(mul(x2, p.ZZ), p.X);   // U2 - X: < 6p
-  F Rd = sub<2>(mul(y2, p.ZZZ), p.Y);  // S2 - Y: < 4p
+// p + (x2, neg ? -y2 : y2): the sign is applied to S2 = y2 ZZZ (one pass: Rd = +-S2 - Y + 4p)
+// instead of negating y2 before the addition (a subtraction pass and a select for every entry)
+SV29_HD Xyzz madd(const Xyzz& p, const F& x2, const F& y2, bool neg) {
+  if (is_identity(p)) return {x2, neg ? sub<2>(zero(), y2) : y2, one(), one()};
+  F Pd = sub<8>(mul(x2, p.ZZ), p.X);                 // U2 - X: < 10p (state X < 8p)
+  F Rd = sub_sgn<4>(mul(y2, p.ZZZ), neg, p.Y);       // +-S2 - Y + 4p: < 6p
   F X = p.X, Y = p.Y, ZZ = p.ZZ, ZZZ = p.ZZZ;
   bool dbl = false;
-  if (is_zero_mod_p_6p(Pd)) {
+  if (is_zero_mod_p_10p(Pd)) {
     if (!is_zero_mod_p_6p(Rd)) return identity();
-    const F x2s = sqr(x2);
-    Pd = add(y2, y2);               // < 4p
+    const F x2s = sqr(x2), ys = neg ? sub<2>(zero(), y2) : y2;
+    Pd = add(ys, ys);               // < 4p
     Rd = add(add(x2s, x2s), x2s);   // < 6p
-    X = x2, Y = y2, ZZ = one(), ZZZ = one();
+    X = x2, Y = ys, ZZ = one(), ZZZ = one();
     dbl = true;
   }
+  // sqr / mul take inputs below 12p: Pd < 10p, X < 8p
   const F PP = sqr(Pd), PPP = mul(Pd, PP), Q = mul(X, PP), R2 = sqr(Rd);  // < 2p
-  // (R2 [+ 2p - PPP]) + 4p - 2Q < 8p -> < 4p
-  const F X3 = csub<4>(sub<4>(dbl ? R2 : sub<2>(R2, PPP), add(Q, Q)));
-  // Y3 = Rd (Q - X3) - Y PPP, one reduction: inputs Rd < 6p, Q + 4p - X3 < 6p, Y < 2p, 2p - PPP
-  const F Y3 = mul_sum2(Rd, sub<4>(Q, X3), Y, sub<2>(zero(), PPP));
+  // X3 = R2 [- PPP] - 2Q + 6p in one pass: in (0, 8p), left there (the next madd's sub<8> and
+  // mul take it; a stored sum is brought below 4p by its writer)
+  const F X3 = sub_2c<6>(R2, dbl ? zero() : PPP, Q);
+  // Y3 = Rd (Q - X3) - Y PPP, one reduction: Rd < 6p, Q + 8p - X3 < 10p, Y < 2p, 2p - PPP < 2p:
+  // 60p^2 + 4p^2 below p R' = 169.6p^2, so the output is below 2p
+  const F Y3 = mul_sum2(Rd, sub<8>(Q, X3), Y, sub<2>(zero(), PPP));
   return {X3, Y3, mul(ZZ, PP), mul(ZZZ, PPP)};
 }
+SV29_HD Xyzz madd(const Xyzz& p, const F& x2, const F& y2) { return madd(p, x2, y2, false); }
 
 // p + q, both XYZZ states (bounds as above; either may be the identity).  add-2008-s; the
 // doubling case (p = q) runs through the same products as in madd: dbl-2008-s-1's U = 2Y, M = 3X²,

@@ -289,6 +289,39 @@ SV29_HD F29<M> add(const F29<M>& a, const F29<M>& b) {
   return r;
 }
 
+// a + K p - b - 2 c in ONE normalized pass (round 5: the XYZZ addition's X3 = R^2 - PPP - 2Q + 6p
+// without its three passes and the conditional subtraction), for normalized b, c and a value in
+// [0, 2^261); a limb's partial sum stays inside int32 (above -3 * 2^29 - 4, below 2^30 + 2)
+template <int K, class M>
+SV29_HD F29<M> sub_2c(const F29<M>& a, const F29<M>& b, const F29<M>& c) {
+  F29<M> r;
+  int32_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < L; i++) {
+    const int32_t x = (int32_t)(a.v[i] + M::kp(K, i)) - (int32_t)b.v[i] - 2 * (int32_t)c.v[i] + cy;
+    cy = x >> 29;  // arithmetic: floor division by 2^29 (-3 .. 1)
+    r.v[i] = (uint32_t)x & MASK;
+  }
+  return r;
+}
+
+// (neg ? -a : a) + K p - b in one normalized pass (round 5: the bucket chain's Rd = +-S2 - Y + 4p,
+// the point's sign applied to S2 instead of negating y2 for every entry), for normalized a, b and a
+// value in [0, 2^261); a limb's partial sum stays inside int32
+template <int K, class M>
+SV29_HD F29<M> sub_sgn(const F29<M>& a, bool neg, const F29<M>& b) {
+  F29<M> r;
+  int32_t cy = 0;
+  const uint32_t sgn = neg ? 0xffffffffu : 1u;
+#pragma unroll
+  for (int i = 0; i < L; i++) {
+    const int32_t x = (int32_t)(a.v[i] * sgn) + (int32_t)M::kp(K, i) - (int32_t)b.v[i] + cy;
+    cy = x >> 29;  // arithmetic: floor division by 2^29 (-2 .. 1)
+    r.v[i] = (uint32_t)x & MASK;
+  }
+  return r;
+}
+
 // a below 2 K p -> below K p: a - K p when that does not go negative
 template <int K, class M>
 SV29_HD F29<M> csub(const F29<M>& a) {
@@ -329,6 +362,18 @@ SV29_HD bool is_zero_mod_p_6p(const F& a) {
   if (!cand) return false;
   // rare: reduce below p by conditional subtractions of 4p, 2p, p (a < 6p < 8p)
   return is_zero(csub<1>(csub<2>(csub<4>(a))));
+}
+
+// a == 0 mod p for a below 10p (round 5: the bucket chain's Pd = U2 - X + 8p with X below 8p)
+SV29_HD bool is_zero_mod_p_10p(const F& a) {
+  constexpr uint32_t LOW[10] = {0u,         0x187cfd47u, 0x10f9fa8eu, 0x976f7d5u,  0x1f3f51cu,
+                                0x1a70f263u, 0x12edefaau, 0xb6aecf1u,  0x3e7ea38u,  0x1c64e77fu};
+  bool cand = false;
+#pragma unroll
+  for (int k = 0; k < 10; k++) cand |= a.v[0] == LOW[k];
+  if (!cand) return false;
+  // rare: reduce below p by conditional subtractions of 8p, 4p, 2p, p (a < 10p < 16p)
+  return is_zero(csub<1>(csub<2>(csub<4>(csub<8>(a)))));
 }
 
 // Form changes without a product: x R' = 32 (x R) mod p, so the way in is a 5-bit shift and a

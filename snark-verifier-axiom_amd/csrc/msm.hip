@@ -842,9 +842,9 @@ struct AccChain<true> {
   __device__ static T in(const G1Xyzz& a) {  // storage form: x R' as words (r29w_*)
     return {r29::from_words(a.X.v), r29::from_words(a.Y.v), r29::from_words(a.ZZ.v), r29::from_words(a.ZZZ.v)};
   }
-  __device__ static G1Xyzz out(const T& a) {
+  __device__ static G1Xyzz out(const T& a) {  // the chain's X may reach 8p: stored below 4p
     G1Xyzz r;
-    r29::to_words(a.X, r.X.v);
+    r29::to_words(r29::csub<4>(a.X), r.X.v);
     r29::to_words(a.Y, r.Y.v);
     r29::to_words(a.ZZ, r.ZZ.v);
     r29::to_words(a.ZZZ, r.ZZZ.v);
@@ -852,7 +852,7 @@ struct AccChain<true> {
   }
   __device__ static G1Xyzz canonical(const T& a) {  // field.hpp's canonical x R form
     G1Xyzz r;
-    r29::to_r32(a.X, r.X.v);
+    r29::to_r32(r29::csub<4>(a.X), r.X.v);
     r29::to_r32(a.Y, r.Y.v);
     r29::to_r32(a.ZZ, r.ZZ.v);
     r29::to_r32(a.ZZZ, r.ZZZ.v);
@@ -860,7 +860,7 @@ struct AccChain<true> {
   }
   __device__ static T madd(const T& acc, const G1Aff& p, bool neg) {
     const r29::F x = r29::from_words(p.x.v), y = r29::from_words(p.y.v);  // the table's x R' words
-    return r29::madd(acc, x, neg ? r29::sub<2>(r29::zero(), y) : y);
+    return r29::madd(acc, x, y, neg);
   }
 };
 

@@ -54,12 +54,14 @@ static F parse(const std::string& h) {
   }
   return r;
 }
-// "madd" mode: stdin lines "X Y ZZ ZZZ x2 y2" (hex) -> "X3 Y3 ZZ3 ZZZ3"
+// "madd" / "maddn" mode: stdin lines "X Y ZZ ZZZ x2 y2" (hex) -> "X3 Y3 ZZ3 ZZZ3" of
+// state + (x2, y2) / state + (x2, -y2)
+static bool g_neg = false;
 static int madd_mode() {
   char buf[6][80];
   while (scanf("%79s %79s %79s %79s %79s %79s", buf[0], buf[1], buf[2], buf[3], buf[4], buf[5]) == 6) {
     const Xyzz st{parse(buf[0]), parse(buf[1]), parse(buf[2]), parse(buf[3])};
-    const Xyzz r = madd(st, parse(buf[4]), parse(buf[5]));
+    const Xyzz r = madd(st, parse(buf[4]), parse(buf[5]), g_neg);
     pr(r.X), pr(r.Y), pr(r.ZZ), pr(r.ZZZ);
     printf("\n");
   }
@@ -94,6 +96,10 @@ static int run_ops(bool fq) {
     pr(a), pr(b), pr(sub<4>(a, b));
     printf("\nsub6");
     pr(a), pr(b), pr(sub<6>(a, b));
+    printf("\nsub8");
+    pr(a), pr(b), pr(sub<8>(a, b));
+    printf("\nsub2c6");
+    pr(a), pr(b), pr(c), pr(sub_2c<6>(a, b, c));
     printf("\ncsub1");
     pr(a), pr(csub<1>(a));
     printf("\ncsub2");
@@ -104,6 +110,9 @@ static int run_ops(bool fq) {
       printf("\nzero6 ");
       pr(a);
       printf(" %d", is_zero_mod_p_6p(a) ? 1 : 0);
+      printf("\nzero10 ");
+      pr(a);
+      printf(" %d", is_zero_mod_p_10p(a) ? 1 : 0);
     }
     uint32_t w[8], w2[8];
     to_words(a, w);
@@ -124,12 +133,17 @@ static int run_ops(bool fq) {
     printf("\n");
   }
   // zero tests on exact multiples of p
-  for (int k = 0; fq && k < 6; k++) {
+  for (int k = 0; fq && k < 10; k++) {
     F m = zero();
     for (int j = 0; j < k; j++) m = sub<1>(m, zero());  // m + p
-    printf("zero6 ");
+    if (k < 6) {
+      printf("zero6 ");
+      pr(m);
+      printf(" %d\n", is_zero_mod_p_6p(m) ? 1 : 0);
+    }
+    printf("zero10 ");
     pr(m);
-    printf(" %d\n", is_zero_mod_p_6p(m) ? 1 : 0);
+    printf(" %d\n", is_zero_mod_p_10p(m) ? 1 : 0);
   }
   return 0;
 }
@@ -149,6 +163,7 @@ static int xadd_mode() {
 
 int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "madd")) return madd_mode();
+  if (argc > 1 && !strcmp(argv[1], "maddn")) return g_neg = true, madd_mode();
   if (argc > 1 && !strcmp(argv[1], "xadd")) return xadd_mode();
   const bool fr = argc > 1 && !strcmp(argv[1], "fr");  // the same checks over Fr (FrM29)
   return fr ? run_ops<FrM29>(false) : run_ops<FqM29>(true);

@@ -63,6 +63,12 @@ def test_field_ops_values_and_bounds(f29, field):
                 want = ins[0] * ins[1] + ins[2] * ins[3]
             assert r < 2 * P, line
             assert r % P == want * RINV % P, line
+        elif op == "sub2c6":
+            a, b, c, r = v
+            want = a + 6 * P - b - 2 * c
+            if not 0 <= want < (1 << 261):
+                continue  # outside the stated contract: not checked
+            assert r == want, line
         elif op.startswith("sub"):
             k = int(op[3:])
             a, b, r = v
@@ -78,9 +84,9 @@ def test_field_ops_values_and_bounds(f29, field):
             if a >= 2 * k * P:
                 continue
             assert r % P == a % P and r < k * P, line
-        elif op == "zero6":
+        elif op in ("zero6", "zero10"):
             a, z = v
-            if a >= 6 * P:
+            if a >= int(op[4:]) * P:
                 continue
             assert z == (1 if a % P == 0 else 0), line
         elif op == "words":
@@ -95,9 +101,11 @@ def test_field_ops_values_and_bounds(f29, field):
             assert r < P and r == a * pow(32, -1, P) % P, line
     assert counts.get("mul", 0) >= 3000 and counts.get("mul_ilp", 0) >= 3000 and counts.get("to_r32", 0) >= 3000 and counts.get("mul_sum3", 0) >= 3000
     assert counts.get("zero6", 0) >= (3006 if field == "fq" else 0)
+    assert counts.get("zero10", 0) >= (3010 if field == "fq" else 0)
+    assert counts.get("sub2c6", 0) >= 3000 and counts.get("sub8", 0) >= 3000
 
 
-def _state(pt, rng, identity=False):
+def _state(pt, rng, identity=False, xmax=4):
     """A random XYZZ representation of an affine point inside the stated bounds (R' form)."""
     if identity:
         return (0, 0, 0, 0)
@@ -106,7 +114,7 @@ def _state(pt, rng, identity=False):
     zz, zzz = z * z % P, z * z * z % P
     X, Y = x * zz % P, y * zzz % P
     m = lambda v: v * RP % P  # noqa: E731
-    return (m(X) + rng.randrange(4) * P, m(Y) + rng.randrange(2) * P, m(zz) + rng.randrange(2) * P,
+    return (m(X) + rng.randrange(xmax) * P, m(Y) + rng.randrange(2) * P, m(zz) + rng.randrange(2) * P,
             m(zzz) + rng.randrange(2) * P)
 
 
@@ -117,8 +125,10 @@ def _to_affine(X, Y, ZZ, ZZZ):
     return (X * pow(ZZ, -1, P) % P, Y * pow(ZZZ, -1, P) % P)
 
 
-def test_madd_group_law(f29):
-    rng = random.Random(29)
+@pytest.mark.parametrize("neg", [False, True])
+def test_madd_group_law(f29, neg):
+    """state + (x2, +-y2): the chain's signed point (neg folds the sign into S2 = y2 ZZZ)."""
+    rng = random.Random(29 + neg)
     g = (1, 2)
     cases = []  # (state, x2, y2, expected affine sum or None)
     for n in range(300):
@@ -129,17 +139,19 @@ def test_madd_group_law(f29):
             b = a  # doubling branch
         elif kind == 8:
             b = ob.g1_neg(a)  # P + (-P)
-        st = _state(a, rng, identity=(kind == 9))
+        st = _state(a, rng, identity=(kind == 9), xmax=8)  # madd's chain state: X below 8p
         want = b if kind == 9 else ob.g1_add(a, b)
+        yv = ob.g1_neg(b)[1] if neg else b[1]  # the point handed over is (x, y) with y negated by neg
         xb = b[0] * RP % P + rng.randrange(2) * P
-        yb = b[1] * RP % P + rng.randrange(2) * P
+        yb = yv * RP % P + rng.randrange(2) * P
         cases.append((st, xb, yb, want))
     inp = "\n".join(" ".join(hex(v) for v in (*st, xb, yb)) for st, xb, yb, _ in cases) + "\n"
-    out = subprocess.run([f29, "madd"], input=inp, capture_output=True, text=True, check=True).stdout.splitlines()
+    out = subprocess.run([f29, "maddn" if neg else "madd"], input=inp, capture_output=True, text=True,
+                         check=True).stdout.splitlines()
     assert len(out) == len(cases)
     for (st, xb, yb, want), line in zip(cases, out):
         X, Y, ZZ, ZZZ = (_limbs(v) for v in line.split())
-        assert X < 4 * P and Y < 2 * P and ZZ < 2 * P and ZZZ < 2 * P, line
+        assert X < 8 * P and Y < 2 * P and ZZ < 2 * P and ZZZ < 2 * P, line  # madd's chain: X < 8p
         got = _to_affine(X, Y, ZZ, ZZZ)
         assert got == (None if want is None else tuple(want)), (st, xb, yb)
         if got is None:

@@ -42,6 +42,39 @@ __global__ void __launch_bounds__(256) k_bench(int op, int iters, unsigned long 
   }
 }
 
+// one operation per kernel (no op switch in the loop): OP as k_bench's op
+template <int OP>
+__global__ void __launch_bounds__(256) k_bench1(int iters, unsigned long long* cycles, uint32_t* sink) {
+  __shared__ Fq2 S[3 * 6];
+  __shared__ Fq gam[3 * 6 * 2];
+  const int t = threadIdx.x;
+  if (t < 6) {
+    S[t] = Fq2::one();
+    S[t].c1 = Fq::one();
+    S[6 + t] = S[t];
+  }
+  for (int i = t; i < 3 * 6 * 16; i += 256) reinterpret_cast<uint32_t*>(gam)[i] = c_gamma[i];
+  __syncthreads();
+  Fq2* a = S;
+  Fq2* b = S + 6;
+  Fq2* c = S + 12;
+  const wg::WLane L = wg::wlane_init();
+  const unsigned long long t0 = clock64();
+  for (int i = 0; i < iters; i++) {
+    if constexpr (OP == 0) wg::w_sqr(L, c, a);
+    else if constexpr (OP == 1) wg::w_mul(L, c, a, b);
+    else wg::w_frob(L, c, a, 1, gam);
+    Fq2* tmp = a;
+    a = c;
+    c = tmp;
+  }
+  const unsigned long long t1 = clock64();
+  if (t == 0) {
+    *cycles = t1 - t0;
+    sink[0] = a[0].c0.v[0];
+  }
+}
+
 // round 5: a product on 8 x 32-bit words computed with field29.hpp's mul_ilp (x R' domain: the words
 // are converted to 9 x 29-bit limbs and back) -- timing only, the domain is not the slots' one
 __device__ __forceinline__ Fq mul29w(const Fq& a, const Fq& b) {
@@ -89,6 +122,49 @@ __device__ __forceinline__ void w_mul_dbg(const wg::WLane& L, Fq2* __restrict__ 
   if (!(mode & 8)) __syncthreads();
 }
 
+// the same switches over round 5's w_mul (lane_sum24): 1 no product, 2 no cross-lane levels (the
+// lane's own split, multiply and normalisation only), 4 no lz_reduce, 8 no barrier, 16 no LDS
+// operand loads; mode bit 64 selects this variant in k_bench_dbg
+__device__ __forceinline__ void w_mul_dbg24(const wg::WLane& L, Fq2* __restrict__ dst, const Fq2* a, const Fq2* b,
+                                            int mode) {
+  using namespace wg;
+  const int t = threadIdx.x;
+  if (t < 192) {
+    const int q = L.mq;
+    Fq ax, by;
+    if (mode & 16) {
+      ax = Fq::one();
+      ax.v[0] ^= t;
+      by = ax;
+    } else {
+      ax = ld_fq((q & 1) ? &a[L.mi].c1 : &a[L.mi].c0);
+      by = ld_fq((q == 1 || q == 2) ? &b[L.mjj].c1 : &b[L.mjj].c0);
+    }
+    const Fq v = (mode & 1) ? ax : fe_mul_lazy(ax, by);
+    Lz s;
+    if (mode & 2) {
+      uint32_t l[kL24], x[kL24];
+      split24(v, l);
+#pragma unroll
+      for (int i = 0; i < kL24; i++) x[i] = L.mkeep * l[i] + L.msend * l[i];
+      s = norm24(x);
+    } else {
+      s = lane_sum24<5>(v, L.mkeep, L.msend);
+    }
+    const int j = t & 31;
+    if (j < 2) {
+      Fq r;
+      if (mode & 4) {
+        for (int x = 0; x < 8; x++) r.v[x] = s.v[x];
+      } else {
+        r = lz_reduce(s);
+      }
+      st_fq(j ? &dst[L.mk].c1 : &dst[L.mk].c0, r);
+    }
+  }
+  if (!(mode & 8)) __syncthreads();
+}
+
 __global__ void __launch_bounds__(256) k_bench_dbg(int mode, int iters, unsigned long long* cycles, uint32_t* sink) {
   __shared__ Fq2 S[3 * 6];
   const int t = threadIdx.x;
@@ -103,7 +179,8 @@ __global__ void __launch_bounds__(256) k_bench_dbg(int mode, int iters, unsigned
   const wg::WLane L = wg::wlane_init();
   const unsigned long long t0 = clock64();
   for (int i = 0; i < iters; i++) {
-    w_mul_dbg(L, c, a, b, mode);
+    if (mode & 64) w_mul_dbg24(L, c, a, b, mode);
+    else w_mul_dbg(L, c, a, b, mode);
     Fq2* tmp = a;
     a = c;
     c = tmp;
@@ -193,7 +270,17 @@ int main() {
     (void)hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
     printf("%-7s %8.1f cycles/op (clock64)\n", names[op], (double)c / iters);
   }
-  for (int mode : {0, 32, 1, 2, 4, 8, 16, 2 | 4, 1 | 2 | 4, 1 | 2 | 4 | 8, 31, 32 | 2 | 4}) {
+  {
+    void (*ks[3])(int, unsigned long long*, uint32_t*) = {k_bench1<0>, k_bench1<1>, k_bench1<2>};
+    for (int op = 0; op < 3; op++) {
+      hipLaunchKernelGGL(ks[op], dim3(1), dim3(256), 0, 0, 4, dc, ds);
+      hipLaunchKernelGGL(ks[op], dim3(1), dim3(256), 0, 0, iters, dc, ds);
+      unsigned long long c = 0;
+      (void)hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
+      printf("%-7s %8.1f cycles/op (alone in its kernel)\n", names[op], (double)c / iters);
+    }
+  }
+  for (int mode : {0, 1, 2, 4, 8, 16, 64, 64 | 1, 64 | 2, 64 | 4, 64 | 8, 64 | 16, 64 | 1 | 2 | 4, 64 | 1 | 2 | 4 | 8, 64 | 31}) {
     hipLaunchKernelGGL(k_bench_dbg, dim3(1), dim3(256), 0, 0, mode, 4, dc, ds);
     hipLaunchKernelGGL(k_bench_dbg, dim3(1), dim3(256), 0, 0, mode, iters, dc, ds);
     unsigned long long c = 0;

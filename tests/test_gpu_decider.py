@@ -219,3 +219,30 @@ def test_gt_equals_halo2curves_structured_restatement(gpu, oracle_cpp):
         _, gt = cpu_ref.count_decide_fpmul_h2c(G2, SG2, L[i], R[i])
         limbs = [sum(int(gt[8 * c + 4 * h + j]) << (64 * j) for j in range(4)) for c in range(6) for h in range(2)]
         assert gts[i] == limbs, i
+
+
+@pytest.mark.parametrize("env", ["SVGPU_DECIDER_WIDE=0", "SVGPU_DECIDER_PAIR=0", "SVGPU_DECIDER_KC=0",
+                                 "SVGPU_DECIDER_WIDE=0 SVGPU_DECIDER_PAIR=0"])
+def test_decider_prologue_variants(gpu, oracle_cpp, monkeypatch, env):
+    """k_decide_wg's prologue options (the round-5 one-term-per-lane products and their round-4
+    form, paired Miller steps, pair products from the key's constants) all give the oracle's Gt
+    values, verdicts and first failure -- identity points included."""
+    import svgpu
+    from svgpu import device as dv
+    from svgpu import encoding as enc
+    for kv in env.split():
+        k, v = kv.split("=")
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("SVGPU_DECIDER_LANES", "256")
+    n = 12
+    g2, sg2, accs = b.gen_decider_case(n, seed=0xC0DE, bad=[7])
+    accs[4] = (None, None)                                      # identity pair: passes
+    accs[9] = (accs[9][0], None)                                # rhs identity: e(lhs, g2) != 1
+    L, R = enc.bases_array([a[0] for a in accs]), enc.bases_array([a[1] for a in accs])
+    ff, verdicts, gts = dv.decide(g2, sg2, _dev([a[0] for a in accs], gpu), _dev([a[1] for a in accs], gpu),
+                                  svgpu.SV_CANONICAL, want_gt=True)
+    eff, egt = oracle_cpp.decide_all(np.frombuffer(b.g2_bytes(g2), np.uint64), np.frombuffer(b.g2_bytes(sg2), np.uint64),
+                                     L, R, threads=0, want_gt=True)
+    assert ff == eff == 7
+    for i in range(n):
+        assert [int(x) for x in gts[i]] == [enc.limbs_to_int(egt[i][4 * c:4 * c + 4]) for c in range(12)], i

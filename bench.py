@@ -471,6 +471,13 @@ def main():
     # instructions per dispatch x 4 clocks over the launch's SIMD-clocks (live kernel time)
     valu = None
     sqf = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_sq_counters.json"))
+    try:  # the SQ pass of the same evidence run as profiles/pmc_accumulate.json (its "source" tag)
+        tag = os.path.basename(json.load(open(os.path.join(ROOT, "profiles", "pmc_accumulate.json")))["source"])
+        tag = tag.replace("_kernel_stats.md", "_sq_counters.json")
+        if tag in sqf:
+            sqf.append(tag)
+    except (OSError, KeyError, ValueError):
+        pass
     if sqf:
         try:
             sqd = json.load(open(os.path.join(ROOT, "profiles", sqf[-1])))

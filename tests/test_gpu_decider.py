@@ -246,3 +246,23 @@ def test_decider_prologue_variants(gpu, oracle_cpp, monkeypatch, env):
     assert ff == eff == 7
     for i in range(n):
         assert [int(x) for x in gts[i]] == [enc.limbs_to_int(egt[i][4 * c:4 * c + 4]) for c in range(12)], i
+
+
+def test_decider_verdict_copy_path(gpu, oracle_cpp, monkeypatch):
+    """SVGPU_DECIDE_ZC=0: verdicts through a device buffer and a copy (the default writes them
+    straight into pinned host memory) -- same first failure and verdicts."""
+    import svgpu
+    from svgpu import device as dv
+    from svgpu import encoding as enc
+    g2, sg2, accs = b.gen_decider_case(10, seed=0xD1CE, bad=[3, 8])
+    L, R = enc.bases_array([a[0] for a in accs]), enc.bases_array([a[1] for a in accs])
+    got = {}
+    for zc in ("1", "0"):
+        monkeypatch.setenv("SVGPU_DECIDE_ZC", zc)
+        ff, verdicts, _ = dv.decide(g2, sg2, _dev([a[0] for a in accs], gpu), _dev([a[1] for a in accs], gpu),
+                                    svgpu.SV_CANONICAL)
+        got[zc] = (ff, verdicts)
+    eff, _ = oracle_cpp.decide_all(np.frombuffer(b.g2_bytes(g2), np.uint64), np.frombuffer(b.g2_bytes(sg2), np.uint64),
+                                   L, R, threads=0, want_gt=False)
+    assert got["1"] == got["0"] and got["1"][0] == eff == 3
+    assert [i for i, v in enumerate(got["1"][1]) if not v] == [3, 8]

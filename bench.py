@@ -375,8 +375,12 @@ def main():
             return parallel.sharded_decide_device(g2, sg2, L, R, rank * dn, svgpu.SV_CANONICAL)
         ff_, _, _ = dv.decide(g2, sg2, L, R)
         return ff_
-    ff = decide_step()
-    dsteps = max(1, args.steps // 2)
+    # the decider line's own loop: a call is ~0.5 ms, so a few warm calls and at least 20 timed ones
+    # (5 right after one call read 0.56 ms per call on a box whose steady state was 0.52)
+    dwarm = max(3, args.warmup)
+    for _ in range(dwarm):
+        ff = decide_step()
+    dsteps = max(20, 2 * args.steps)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -527,6 +531,7 @@ def main():
             "checks_per_s": pairings_per_s / 2,
             "accumulators_per_gpu": dn,
             "ms_per_decide_all": dec_s / dsteps * 1e3,
+            "calls": {"warmup": dwarm, "timed": dsteps},
             "kernel_ms": float(np.mean(dec_kernel_ms)),
             "first_fail": ff,
             "fpmul_per_check": {"h2c_restatement_counted": FPMUL_H2C_COUNTED,

@@ -1527,7 +1527,9 @@ int decide_run_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const vo
   int32_t* d_verdict = zc ? nullptr : ws->carve<int32_t>(n);
   if (zc) SV_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_verdict), ws->pinned, 0));
   Fq12* d_gt = gt_host ? ws->carve<Fq12>(n) : nullptr;
-  SV_HIP(hipEventRecord(ws->ev[0], st));
+  // kernel timing events (sv_decide_last_kernel_ms); SVGPU_DECIDE_EVENTS=0 leaves them out (read per call)
+  const bool timed = !getenv("SVGPU_DECIDE_EVENTS") || atoi(getenv("SVGPU_DECIDE_EVENTS")) != 0;
+  if (timed) SV_HIP(hipEventRecord(ws->ev[0], st));
   // SVGPU_DECIDER_LANES = 48 (6 x 8 lanes per accumulator, 1 per wave; default) or 24 (6 x 4, 2 per wave)
   // SVGPU_DECIDER_LANES: 256 = k_decide_wg (one 4-wave block per accumulator: lowest latency, one
   // block per CU), 48 / 24 = k_decide_lanes (one wave per accumulator, two blocks per CU: higher
@@ -1567,7 +1569,7 @@ int decide_run_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const vo
     hipLaunchKernelGGL(k_decide_lanes<4>, dim3((unsigned)((n + 1) / 2)), dim3(64), 0, st, dl, dr, (uint32_t)n,
                        lines, L2, mont, d_verdict, d_gt, phases);
   SV_HIP(hipGetLastError());
-  SV_HIP(hipEventRecord(ws->ev[1], st));
+  if (timed) SV_HIP(hipEventRecord(ws->ev[1], st));
   int32_t* hv = reinterpret_cast<int32_t*>(ws->pinned);
   if (!zc) SV_HIP(hipMemcpyAsync(hv, d_verdict, n * 4, hipMemcpyDeviceToHost, st));
   if (gt_host) {
@@ -1585,8 +1587,8 @@ int decide_run_device(const sv_g2_affine* g2, const sv_g2_affine* s_g2, const vo
     }
   }
   SV_HIP(hipStreamSynchronize(st));
-  float ms = 0;
-  (void)hipEventElapsedTime(&ms, ws->ev[0], ws->ev[1]);
+  float ms = -1;
+  if (timed) (void)hipEventElapsedTime(&ms, ws->ev[0], ws->ev[1]);
   decider_last_kernel_ms() = ms;
   int32_t ff = -1;
   for (size_t i = 0; i < n; i++) {

@@ -49,3 +49,19 @@ def test_g2_cache_key_accepts_nested_lists():
     c = dv._g2_struct_cached(q, 0)
     assert bytes(a) == bytes(c)
     assert dv._g2_struct_cached(as_lists, 0) is a or bytes(dv._g2_struct_cached(as_lists, 0)) == bytes(a)
+
+
+def test_g2_cache_identity_fast_path_sees_mutation():
+    """The identity-keyed fast path (the same key object passed again) returns the cached struct only
+    while the object's contents are unchanged: a list mutated in place gets the new point's struct."""
+    from svgpu import device as dv
+    from svgpu import encoding as enc
+    from oracle import bn254 as b
+    q, s = b.G2_GEN, b.g2_mul(b.G2_GEN, 5)
+    key = [[q[0][0], q[0][1]], [q[1][0], q[1][1]]]
+    first = dv._g2_struct_cached(key, 0)
+    assert dv._g2_struct_cached(key, 0) is first
+    key[0][0], key[0][1], key[1][0], key[1][1] = s[0][0], s[0][1], s[1][0], s[1][1]
+    assert bytes(dv._g2_struct_cached(key, 0)) == bytes(enc.g2_struct(s, 0))
+    arr = [list(map(int, c)) for c in q]
+    assert bytes(dv._g2_struct_cached(arr, 1)) == bytes(enc.g2_struct(arr, 1))

@@ -12,17 +12,17 @@ from oracle import bn254 as ob
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NATIVE = os.path.join(ROOT, "tests", "native")
-BIN = os.path.join(NATIVE, "build", "field29check")
 P = ob.P
 RP = (1 << 261) % P  # R' = 2^261
 RINV = pow(RP, -1, P)
 
 
-@pytest.fixture(scope="module")
-def f29():
-    r = subprocess.run(["make", "-s", "-C", NATIVE, "build/field29check"], capture_output=True, text=True)
+@pytest.fixture(scope="module", params=["field29check", "field29check_asan"])
+def f29(request):
+    """The harness as built, and again under ASan + UBSan (any report fails the run)."""
+    r = subprocess.run(["make", "-s", "-C", NATIVE, "build/" + request.param], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
-    return BIN
+    return os.path.join(NATIVE, "build", request.param)
 
 
 def _limbs(h):

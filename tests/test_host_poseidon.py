@@ -12,14 +12,14 @@ from oracle import poseidon as op
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NATIVE = os.path.join(ROOT, "tests", "native")
-BIN = os.path.join(NATIVE, "build", "host_sponge")
 
 
-@pytest.fixture(scope="module")
-def sponge_bin():
-    r = subprocess.run(["make", "-s", "-C", NATIVE, "build/host_sponge"], capture_output=True, text=True)
+@pytest.fixture(scope="module", params=["host_sponge", "host_sponge_asan"])
+def sponge_bin(request):
+    """The harness as built, and again under ASan + UBSan (any report fails the run)."""
+    r = subprocess.run(["make", "-s", "-C", NATIVE, "build/" + request.param], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
-    return BIN
+    return os.path.join(NATIVE, "build", request.param)
 
 
 def _run(binary, state, elements):

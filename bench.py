@@ -550,7 +550,7 @@ def main():
         "breakdown_ms": {k: round(stats[k], 4) for k in
                          ("sort_ms", "accumulate_ms", "reduce_ms", "host_ms", "total_ms")},
         "breakdown_note": "HIP events on the library stream: sort_ms = digit extraction + two-level counting sort "
-                          "(digits never stored), reduce_ms = bucket fixup + reduction, host_ms = host Horner; "
+                          "(digits never stored; the GLV halves kept for the scatter pass), reduce_ms = bucket fixup + reduction, host_ms = host Horner; "
                           "finer splits with SVGPU_MSM_STATS=1 (each extra event costs ~5 us of GPU idle)",
         "roofline": {
             "bound": "hbm",

@@ -239,6 +239,31 @@ struct Digits {
       sgn[0] = 0;
     }
   }
+  // The histogram pass stores what load() derived (GLV: both halves, the sign in bit 31 of the top
+  // word; else the canonical scalar): 32 B per point, so the scatter pass reads it back instead of
+  // converting from Montgomery form and splitting again (SVGPU_SORT_HALVES=0: recompute, as before)
+  __device__ __forceinline__ void store(uint4* __restrict__ hv, uint32_t i) const {
+    if constexpr (GLV) {
+      hv[2 * i] = make_uint4(h[0][0], h[0][1], h[0][2], h[0][3] | (sgn[0] << 31));
+      hv[2 * i + 1] = make_uint4(h[1][0], h[1][1], h[1][2], h[1][3] | (sgn[1] << 31));
+    } else {
+      hv[2 * i] = make_uint4(h[0][0], h[0][1], h[0][2], h[0][3]);
+      hv[2 * i + 1] = make_uint4(h[0][4], h[0][5], h[0][6], h[0][7]);
+    }
+  }
+  __device__ __forceinline__ void load_stored(const uint4* __restrict__ hv, uint32_t i) {
+    const uint4 a = hv[2 * i], b = hv[2 * i + 1];
+    if constexpr (GLV) {
+      h[0][0] = a.x; h[0][1] = a.y; h[0][2] = a.z; h[0][3] = a.w & 0x7fffffffu;
+      h[1][0] = b.x; h[1][1] = b.y; h[1][2] = b.z; h[1][3] = b.w & 0x7fffffffu;
+      sgn[0] = a.w >> 31;
+      sgn[1] = b.w >> 31;
+    } else {
+      h[0][0] = a.x; h[0][1] = a.y; h[0][2] = a.z; h[0][3] = a.w;
+      h[0][4] = b.x; h[0][5] = b.y; h[0][6] = b.z; h[0][7] = b.w;
+      sgn[0] = 0;
+    }
+  }
   template <class F>
   __device__ __forceinline__ void each(F&& f) const {
 #pragma unroll
@@ -435,7 +460,8 @@ __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scal
                                                      uint32_t nblk, uint32_t* __restrict__ bcnt,
                                                      uint32_t* __restrict__ err, const G1Aff* __restrict__ bases,
                                                      uint4* __restrict__ phix, int phi64, int check_bases,
-                                                     int xcd, int bm, uint32_t w0, uint32_t nw) {
+                                                     int xcd, int bm, uint32_t w0, uint32_t nw,
+                                                     uint4* __restrict__ stored) {
   using D = Digits<C, GLV>;
   constexpr int W = D::W, LOGB = C - 1;
   constexpr int CB = coarse_bits(C, D::NB), FB = LOGB - CB, NBIN = 1 << CB;
@@ -462,6 +488,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scal
     }
     D d;
     d.load(scalars, i, mont_in, err);
+    if (stored) d.store(stored, i);
     d.each([&](int w, uint32_t mag, uint32_t, uint32_t) {
       if (mag && (uint32_t)w - w0 < nw) atomicAdd(&h[(w - w0) * NBIN + ((mag - 1) >> FB)], 1u);
     });
@@ -578,7 +605,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
                                                         const uint32_t* __restrict__ btot,
                                                         const uint32_t* __restrict__ bstart,
                                                         uint64_t* __restrict__ tmp, int e32, int xcd, int bm,
-                                                        uint32_t w0, uint32_t nw) {
+                                                        uint32_t w0, uint32_t nw, const uint4* __restrict__ stored) {
   using D = Digits<C, GLV>;
   constexpr int W = D::W, LOGB = C - 1;
   constexpr int CB = coarse_bits(C, D::NB), FB = LOGB - CB, NBIN = 1 << CB, NK = W * NBIN;
@@ -605,7 +632,10 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(const Fr* __restrict__ s
 #pragma unroll
   for (int j = 0; j < (int)PT; j++) {
     const uint32_t i = lo + threadIdx.x + j * kBlock;
-    if (i < hi) dg[j].load(scalars, i, mont_in, nullptr);
+    if (i < hi) {
+      if (stored) dg[j].load_stored(stored, i);  // written by this sort's k_bin_hist
+      else dg[j].load(scalars, i, mont_in, nullptr);
+    }
   }
   __syncthreads();
   const uint32_t total = block_excl_scan<NK>(off, part);
@@ -1650,7 +1680,7 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
                     const Fr* scalars, size_t m, int mont_in, int device, hipStream_t st, uint4* phix,
                     uint32_t nsplit, int check_bases, hipEvent_t ev_sort_mid, hipStream_t side = nullptr,
                     hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr, uint32_t w0 = 0,
-                    uint32_t nw = 0) {
+                    uint32_t nw = 0, uint4* stored = nullptr) {
   const int LOGB = p.c - 1;
   const int nb = p.glv ? 128 : 255;
   const uint32_t CB = (uint32_t)coarse_bits(p.c, nb), FB = (uint32_t)LOGB - CB, NBIN = 1u << CB;
@@ -1667,7 +1697,7 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
   // block-major per-block counts + the tiled scan (SVGPU_SORT_BM=0: key-major, k_bin_scan_chunks)
   static const int bm = !getenv("SVGPU_SORT_BM") || atoi(getenv("SVGPU_SORT_BM")) != 0 ? 1 : 0;
   SV_LAUNCH_C(k_bin_hist, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.err, bases,
-              phix, p.r29 ? kPhiVtab : p.phi64, check_bases, xcd, bm, w0, nw);
+              phix, p.r29 ? kPhiVtab : p.phi64, check_bases, xcd, bm, w0, nw, stored);
   SV_HIP(hipGetLastError());
   if (ev_sort_mid) SV_HIP(hipEventRecord(ev_sort_mid, st));
   if (bm) {
@@ -1684,7 +1714,7 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
   // measured 12 -> 122 us for that kernel: the fence writes back the XCD's L2)
   hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, st, w.btot, nwb, w.bstart, so.gst + (size_t)nw * p.B);
   SV_LAUNCH_C(k_bin_scatter, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.btot, w.bstart,
-              w.tmp, e32, xcd, bm, w0, nw);
+              w.tmp, e32, xcd, bm, w0, nw, stored);
   static thread_local int fine_attr_dev = -1;  // the > 64 KiB dynamic-LDS opt-in, once per thread/device
   if (fine_attr_dev != device) {
     SV_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fine_sort<0>),
@@ -1903,6 +1933,11 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   add((size_t)nwb * 4);                       // btot
   add(((size_t)nwb + 1) * 4);                 // bstart
   add(piece_entries * 8);                     // tmp (coarse-binned entries)
+  // the histogram pass's digits source for the scatter (32 B per point; the device path without
+  // window halves only; SVGPU_SORT_HALVES=0, read per call: recomputed by the scatter instead)
+  const char* sh_env = getenv("SVGPU_SORT_HALVES");
+  const bool keep_halves = !feed && !split && !(sh_env && atoi(sh_env) == 0);
+  if (keep_halves) add(n * 32);
   add((((size_t)p.nbt + 1) * pieces + 1) * 4);  // gst per piece (+ 1: two window halves)
   add(entries * 4);                           // ent (every piece's sorted entries)
   add(tst_total * 4);                         // tstart per piece
@@ -1939,6 +1974,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   w.btot = ws->carve<uint32_t>(nwb);
   w.bstart = ws->carve<uint32_t>((size_t)nwb + 1);
   w.tmp = ws->carve<uint64_t>(piece_entries);
+  uint4* stored = keep_halves ? ws->carve<uint4>(2 * n) : nullptr;
   uint32_t* gst_all = ws->carve<uint32_t>(((size_t)p.nbt + 1) * pieces + 1);
   uint32_t* ent_all = ws->carve<uint32_t>(entries);
   uint32_t* tst_all = ws->carve<uint32_t>(tst_total);
@@ -2034,7 +2070,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
       half_gst[1] = sh[1].gst;
     } else {
       SV_TRY(msm_sort(p, w, so[0], bases, scalars, n, mont_in, device, st, phix, nsplit, mont_in,
-                      detail ? ev[1] : nullptr, side, ev[60], ev[61]));
+                      detail ? ev[1] : nullptr, side, ev[60], ev[61], 0, 0, stored));
       SV_HIP(hipEventRecord(ev[2], st));
       SV_TRY(msm_acc(p, w, so[0], bases, 0, st, bsum, phix, nsplit, ev[3], detail ? ev[4] : nullptr));
     }

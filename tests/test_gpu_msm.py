@@ -71,6 +71,32 @@ def test_random_sizes_vs_cpp_pippenger(gpu, oracle_cpp, n):
     assert dv.msm(Bd, Sd, svgpu.SV_CANONICAL) == exp
 
 
+@pytest.mark.parametrize("halves", ["0", "1"])
+@pytest.mark.parametrize("glv", ["0", "1"])
+def test_sort_stored_halves(gpu, oracle_cpp, monkeypatch, halves, glv):
+    """The device path's scatter pass reading the digits source the histogram pass stored (GLV
+    halves with their signs, or the canonical scalar) against recomputing it, both input forms
+    (Montgomery scalars are converted by the histogram pass), with edge scalars mixed in."""
+    from svgpu import device as dv
+    from svgpu import encoding as enc
+    import svgpu
+    monkeypatch.setenv("SVGPU_SORT_HALVES", halves)
+    monkeypatch.setenv("SVGPU_GLV", glv)
+    n = 40000
+    B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=5 * n)
+    S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=5 * n)
+    edge = [0, 1, 2, b.R - 1, b.R - 2, (b.R - 1) // 2, 1 << 127, (1 << 127) - 1, 1 << 128, b.R >> 1]
+    S[:len(edge)] = enc.scalars_array(edge)
+    exp = _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
+    Bd = torch.from_numpy(B.view(np.int64)).to(gpu)
+    Sd = torch.from_numpy(S.view(np.int64)).to(gpu)
+    assert dv.msm(Bd, Sd, svgpu.SV_CANONICAL) == exp
+    Sm = enc.scalars_array([enc.limbs_to_int(r) for r in S], svgpu.SV_MONTGOMERY)
+    Bm = enc.bases_array([enc.g1_from_limbs(r) for r in B], svgpu.SV_MONTGOMERY)
+    assert dv.msm(torch.from_numpy(Bm.view(np.int64)).to(gpu), torch.from_numpy(Sm.view(np.int64)).to(gpu),
+                  svgpu.SV_MONTGOMERY) == exp
+
+
 def test_adversarial_single_bucket(gpu, oracle_cpp):
     """All scalars equal: every window's digits land in ONE bucket (maximal bucket skew)."""
     import svgpu

@@ -71,17 +71,21 @@ def test_random_sizes_vs_cpp_pippenger(gpu, oracle_cpp, n):
     assert dv.msm(Bd, Sd, svgpu.SV_CANONICAL) == exp
 
 
+@pytest.mark.parametrize("bits", ["", "10"])
 @pytest.mark.parametrize("halves", ["0", "1"])
 @pytest.mark.parametrize("glv", ["0", "1"])
-def test_sort_stored_halves(gpu, oracle_cpp, monkeypatch, halves, glv):
+def test_sort_stored_halves(gpu, oracle_cpp, monkeypatch, halves, glv, bits):
     """The device path's scatter pass reading the digits source the histogram pass stored (GLV
     halves with their signs, or the canonical scalar) against recomputing it, both input forms
-    (Montgomery scalars are converted by the histogram pass), with edge scalars mixed in."""
+    (Montgomery scalars are converted by the histogram pass), with edge scalars mixed in, at the
+    default window and at 10-bit windows (256-point sort blocks)."""
     from svgpu import device as dv
     from svgpu import encoding as enc
     import svgpu
     monkeypatch.setenv("SVGPU_SORT_HALVES", halves)
     monkeypatch.setenv("SVGPU_GLV", glv)
+    if bits:  # more windows: 256-point sort blocks once a point has more than 20 entries
+        monkeypatch.setenv("SVGPU_WINDOW_BITS", bits)
     n = 40000
     B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=5 * n)
     S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=5 * n)

@@ -7,10 +7,11 @@
 // Pipeline (all on one stream, inputs already in HBM):
 //   k_to_mont_bases   (canonical input only) bases -> Montgomery workspace copy
 //   k_bin_hist        per block of sort_chunk points (1024 at 2^20; XCD-aware block map, sort_block): signed c-bit digits of every
-//                     window (never stored; GLV halves split on the fly) + the phi(P) table, LDS
+//                     window (digits never stored; the GLV halves are, 32 B per point, for the scatter)
+//                     + the point table, LDS
 //                     histogram of (window, coarse bin = top bits of the bucket)
 //   k_bin_scan_chunks / k_bin_scan   offsets of every (window, bin, block) run
-//   k_bin_scatter     digits again; entries appended to their block's (window, bin) run -> tmp
+//   k_bin_scatter     digits again (from the stored halves); entries appended to their block's (window, bin) run -> tmp
 //   k_fine_sort<2>    one block per (window, bin), both region kinds in one launch: counting sort
 //                     by the fine bucket index inside the bin's L2-resident region -> ent[], bucket
 //                     offsets gst[], owner bucket of every accumulate chunk tstart[]
@@ -209,8 +210,8 @@ __device__ __forceinline__ Fr load_scalar(const Fr* __restrict__ scalars, uint32
 }
 
 // Entries of real point i for the sort passes.  Without GLV: the W signed digits of its scalar,
-// all for virtual point i (half 0).  With GLV the scalar is split here (glv.hpp; nothing is
-// stored): the W digits of k1 belong to virtual point i (P_i, half 0) and the W digits of k2 to
+// all for virtual point i (half 0).  With GLV the scalar is split here (glv.hpp; the halves
+// are stored for the scatter pass on the device path, see store()): the W digits of k1 belong to virtual point i (P_i, half 0) and the W digits of k2 to
 // virtual point n + i (phi(P_i), half 1), each half's sign folded into its digits' signs; both
 // halves share the W windows' buckets.  f(w, mag, neg, half) per digit.
 template <int C, bool GLV>
@@ -373,7 +374,7 @@ __global__ void k_check_bases(const G1Aff* __restrict__ bases, uint32_t n, uint3
 // Bucket b = |digit| - 1 of window w splits into a coarse bin b >> FB (NBIN = 2^CB bins per window)
 // and a fine index b & (2^FB - 1).  Pass 1 (k_bin_hist): per block of sort_chunk(c) points, every
 // window's digits, LDS histogram of (window, bin).  Pass 2 (k_bin_scan_chunks, k_bin_scan): global
-// offsets of every (window, bin, block) run.  Pass 3 (k_bin_scatter): the digits again, each
+// offsets of every (window, bin, block) run.  Pass 3 (k_bin_scatter): the digits again (from the halves pass 1 stored), each
 // entry appended to its block's run -> tmp (u64: fine << 32 | point | sign << 31); a block's runs
 // are short contiguous spans, so writes merge in L2.  Pass 4 (k_fine_sort): one block per
 // (window, bin) counting-sorts its ~n / NBIN entries by fine index inside that bin's region (L2
@@ -2269,7 +2270,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   float ms = 0;
   if (detail && !feed) {
     (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
-    s.digits_ms = ms;  // digits + coarse histogram (digits are recomputed, never stored)
+    s.digits_ms = ms;  // digits + coarse histogram (digits never stored; the GLV halves are)
     (void)hipEventElapsedTime(&ms, ev[1], ev[2]);
     s.sort_ms = ms;
     (void)hipEventElapsedTime(&ms, ev[3], ev[4]);

@@ -23,6 +23,7 @@
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "curve.hpp"
 #include "glv.hpp"
@@ -1019,7 +1020,10 @@ __global__ void __launch_bounds__(kThreads) k_msm_batch_fixed(const G1Aff* __res
 
 }  // namespace
 
-static std::atomic<uint64_t> g_fused_redone{0};  // fused launches redone by the two-kernel path
+static std::atomic<uint64_t> g_fused_redone{0};
+int msm_batch_windows_host(const void* d_bases, const void* d_scalars, const uint64_t* d_offsets, size_t count,
+                           size_t max_terms, int scalar_form, int base_form, int device, hipStream_t stream,
+                           host::Xyzz* out);  // fused launches redone by the two-kernel path
 
 int msm_batch_window_bits(size_t max_terms) {
   if (const char* e = getenv("SVGPU_BATCH_WINDOW_BITS")) {
@@ -1029,6 +1033,43 @@ int msm_batch_window_bits(size_t max_terms) {
   return max_terms <= 256 ? 5 : 8;
 }
 
+// Small plain batches (round 5): the window sums on the device and one host Horner per MSM on the
+// host pool (msm_batch_windows_host) instead of the fused kernel, whose one-wave Horner chain takes
+// ~0.65 ms whatever the batch size (one 64-term MSM as long as 128 of them,
+// profiles/r05_batch_floor_probe.log).  The host costs ~35 us per MSM, spread over the pool:
+// 0.17-0.20 ms for 1-16 MSMs of 64 terms, 0.47 at 64, even at ~100, slower at 128
+// (profiles/r05_batch_host_route_ab.log).  SVGPU_BATCH_HOST_MAX sets the largest such batch (0: never).
+constexpr size_t kBatchHostMax = 64;
+static int msm_batch_small_host(const void* d_bases, const void* d_scalars, const uint64_t* d_offsets, size_t count,
+                                size_t max_terms, int form, int device, hipStream_t stream, void* d_out) {
+  std::vector<host::Xyzz> acc(count);
+  SV_TRY(msm_batch_windows_host(d_bases, d_scalars, d_offsets, count, max_terms, form, form, device, stream,
+                                acc.data()));
+  // affine in `form` with ONE inversion (Montgomery's trick over the ZZZ of the non-identity sums):
+  // x = X / ZZ = X (ZZ ZZZ^-1)^2, y = Y / ZZZ; the identity is (0, 0)
+  std::vector<host::F> pre(count);
+  host::F run = host::f_one();
+  for (size_t k = 0; k < count; k++) {
+    pre[k] = run;  // product of the earlier non-identity ZZZ
+    if (!host::x_is_identity(acc[k])) run = host::f_mul(run, acc[k].ZZZ);
+  }
+  host::F inv = host::f_inv(run);
+  std::vector<uint64_t> h(8 * count, 0);
+  for (size_t k = count; k-- > 0;) {
+    if (host::x_is_identity(acc[k])) continue;
+    const host::F izzz = host::f_mul(inv, pre[k]);
+    inv = host::f_mul(inv, acc[k].ZZZ);
+    const host::F iz = host::f_mul(izzz, acc[k].ZZ);
+    host::F x = host::f_mul(acc[k].X, host::f_sqr(iz)), y = host::f_mul(acc[k].Y, izzz);
+    if (form != SV_MONTGOMERY) x = host::f_from_mont(x), y = host::f_from_mont(y);
+    memcpy(&h[8 * k], x.l, 32);
+    memcpy(&h[8 * k + 4], y.l, 32);
+  }
+  SV_HIP(hipSetDevice(device));
+  SV_HIP(hipMemcpy(d_out, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+  return SV_OK;
+}
+
 int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t* d_offsets, const uint32_t* d_ids,
                      size_t count, size_t max_terms, int form, int device, hipStream_t stream, void* d_out,
                      const uint32_t* d_bidx, uint64_t table_len, int base_form) {
@@ -1036,6 +1077,13 @@ int msm_batch_device(const void* d_bases, const void* d_scalars, const uint64_t*
   if (count > 0x7fffffffull) {
     set_error("msm_batch: count = %zu too large", count);
     return SV_ERR_LEN;
+  }
+  {
+    const char* hm = getenv("SVGPU_BATCH_HOST_MAX");  // read per call
+    const size_t host_max = hm ? (size_t)strtoull(hm, nullptr, 10) : kBatchHostMax;
+    if (!d_ids && !d_bidx && count <= host_max && max_terms >= 1 && max_terms <= (size_t)kQMaxTerms &&
+        msm_batch_window_bits(max_terms) == kQC)
+      return msm_batch_small_host(d_bases, d_scalars, d_offsets, count, max_terms, form, device, stream, d_out);
   }
   WsLease lease(device, stream);
   if (!lease.ok()) return SV_ERR_DEVICE;

@@ -240,3 +240,32 @@ def test_fused_wait_timeout_is_redone(gpu, oracle_cpp, monkeypatch):
     assert svgpu.msm_batch_arrays(B, S, off) == exp
     monkeypatch.delenv("SVGPU_BATCH_WAIT_SPINS")
     assert svgpu.msm_batch_arrays(B, S, off) == exp
+
+
+@pytest.mark.parametrize("host_max", ["0", "64"])
+@pytest.mark.parametrize("form", ["canonical", "montgomery"])
+def test_device_small_batch_host_horner(gpu, oracle_cpp, monkeypatch, host_max, form):
+    """Small plain batches (<= SVGPU_BATCH_HOST_MAX MSMs of <= 256 terms) take the window sums on the
+    device and the Horners on the host (one batch inversion for the affine outputs); 0 keeps the
+    fused kernel.  Ragged sizes, an all-zero-scalar MSM (identity out), both forms, batches just
+    inside and outside the default limit."""
+    import svgpu
+    from svgpu import device as dv
+    from svgpu import encoding as enc
+    monkeypatch.setenv("SVGPU_BATCH_HOST_MAX", host_max)
+    f = svgpu.SV_MONTGOMERY if form == "montgomery" else svgpu.SV_CANONICAL
+    for sizes in ([64], [1, 2, 64, 3], [17] * 64, [5] * 65, [256, 1, 255]):
+        B, S, off = _ragged(oracle_cpp, sizes, 123 + len(sizes))
+        if len(sizes) > 1:
+            S[off[1]:off[2]] = 0  # the second MSM sums to the identity
+        exp = _expected(oracle_cpp, B, S, off)
+        if f == svgpu.SV_MONTGOMERY:
+            B = enc.bases_array([enc.g1_from_limbs(r) for r in B], f)
+            S = enc.scalars_array([enc.limbs_to_int(r) for r in S], f)
+        Bd = torch.from_numpy(B.view(np.int64)).to(gpu)
+        Sd = torch.from_numpy(S.view(np.int64)).to(gpu)
+        od = torch.tensor(off, dtype=torch.int64, device=gpu)
+        out = dv.msm_batch(Bd, Sd, od, max(sizes), f)
+        torch.cuda.synchronize()
+        got = [enc.g1_from_limbs(r, f) for r in out.cpu().numpy().view(np.uint64)]
+        assert got == exp, sizes

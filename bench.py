@@ -103,6 +103,21 @@ def next_rows(dev, dv, ob, enc, g2, sg2, accs):
     off = torch.arange(0, count * m + 1, m, dtype=torch.int64, device=dev)
     t, _ = _time(lambda: dv.msm_batch(B, S, off, m, M), 5)
     res["msm_batch"] = {"msms": count, "terms_each": m, "ms": t * 1e3, "terms_per_s": count * m / t}
+    # a few proofs' MSMs (8 x 64 terms): the small-batch route, window sums on the device and the
+    # Horners on the host (SVGPU_BATCH_HOST_MAX), against the fused kernel's one-wave chain
+    small = {}
+    for route, hm in (("host_horner", None), ("fused", "0")):
+        old = os.environ.pop("SVGPU_BATCH_HOST_MAX", None)
+        if hm is not None:
+            os.environ["SVGPU_BATCH_HOST_MAX"] = hm
+        ts, _ = _time(lambda: dv.msm_batch(B, S, off[:9], m, M), 5)
+        small[route] = ts * 1e3
+        os.environ.pop("SVGPU_BATCH_HOST_MAX", None)
+        if old is not None:
+            os.environ["SVGPU_BATCH_HOST_MAX"] = old
+    same_small = bool(torch.equal(dv.msm_batch(B, S, off[:9], m, M), dv.msm_batch(B, S, off, m, M)[:8]))
+    res["msm_batch_small"] = {"msms": 8, "terms_each": m, "ms": small["host_horner"], "fused_ms": small["fused"],
+                              "same_result_as_fused_batch": same_small}
     # f1 with fixed bases: the same batch, each term referencing a row of a 4096-row base table
     #   (created once, rows precomputed as 2^(8w) P: one bucket set per MSM, no window Horner)
     rows = 4096

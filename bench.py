@@ -92,6 +92,64 @@ def _time(fn, reps):
     return float(np.median(ts)), r
 
 
+CROSSOVER_SIZES = (1, 2, 3, 4, 8, 16, 32, 64)
+
+
+def verifier_msm_rows(ob):
+    """The native verifier's own MSMs: a handful of tens-term MSMs per proof (bdfg21.rs:75-78,
+    gwc19.rs:76-79, reached from snark-verifier-sdk/src/halo2/aggregation.rs:219-233), each one
+    NativeLoader::multi_scalar_multiplication call (native.rs:61-71).  (1) The crossover: one
+    reference-shaped library call (sv_bn254_g1_msm_refs, host references, gather + transfer + the
+    small-MSM window path) against the reference's naive sum of scalar muls (the C++ restatement,
+    one thread) per size.  (2) 128 MSMs of 30 terms through 128 sequential calls and through one
+    host-array batch call (sv_bn254_g1_msm_batch), against the naive CPU path."""
+    import svgpu
+    from oracle import cpu_ref
+    C = svgpu.SV_CANONICAL
+    count, m = 128, 30
+    hb = cpu_ref.gen_bases(ob.SEED_BASES, count * m, start=31337)
+    hs = cpu_ref.gen_scalars(ob.SEED_SCALARS, count * m, start=31337)
+
+    def refs_of(lo, hi):
+        idx = np.arange(lo, hi, dtype=np.uint64)
+        return svgpu.make_refs(hs.ctypes.data + 32 * idx, hb.ctypes.data + 64 * idx)
+
+    def med(fn, reps):
+        fn()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)) * 1e3
+    cross = []
+    for k in CROSSOVER_SIZES:
+        rk = refs_of(0, k)
+        g_ms = med(lambda: svgpu.msm_refs(rk, C), 25)
+        c_ms = med(lambda: cpu_ref.msm_naive(hb[:k], hs[:k]), 3)
+        cross.append({"terms": k, "gpu_call_ms": g_ms, "cpu_naive_ms": c_ms})
+    faster = [c["terms"] for c in cross if c["gpu_call_ms"] < c["cpu_naive_ms"]]
+    refs = [refs_of(i * m, (i + 1) * m) for i in range(count)]
+    seq_ms = med(lambda: [svgpu.msm_refs(r, C) for r in refs], 3)
+    off = list(range(0, count * m + 1, m))
+    batch_ms = med(lambda: svgpu.msm_batch_arrays(hb, hs, off, C), 5)
+    batch8_ms = med(lambda: svgpu.msm_batch_arrays(hb[:8 * m], hs[:8 * m], off[:9], C), 10)
+    t0 = time.perf_counter()
+    exp = [ob.g1_from_bytes(cpu_ref.msm_naive(hb[i * m:(i + 1) * m], hs[i * m:(i + 1) * m]).tobytes())
+           for i in range(count)]
+    cpu_ms = (time.perf_counter() - t0) * 1e3
+    same = (svgpu.msm_batch_arrays(hb, hs, off, C) == exp
+            and [svgpu.msm_refs(r, C) for r in refs[:8]] == exp[:8])
+    return {"crossover": cross, "gpu_faster_from_terms": min(faster) if faster else None,
+            "msms": count, "terms_each": m, "sequential_calls_ms": seq_ms, "one_batch_call_ms": batch_ms,
+            "batch_of_8_ms": batch8_ms, "cpu_naive_1_thread_ms": cpu_ms,
+            "x_vs_cpu_sequential": cpu_ms / seq_ms, "x_vs_cpu_batch": cpu_ms / batch_ms,
+            "parity_vs_oracle": bool(same),
+            "note": "host arrays, canonical form; sequential = one sv_bn254_g1_msm_refs call per MSM (what the "
+                    "Rust shim's NativeLoader routing issues); batch = sv_bn254_g1_msm_batch; CPU = the naive "
+                    "NativeLoader restatement (one scalar mul + add per term) on one thread"}
+
+
 def next_rows(dev, dv, ob, enc, g2, sg2, accs):
     import svgpu
     M = svgpu.SV_MONTGOMERY
@@ -118,6 +176,7 @@ def next_rows(dev, dv, ob, enc, g2, sg2, accs):
     same_small = bool(torch.equal(dv.msm_batch(B, S, off[:9], m, M), dv.msm_batch(B, S, off, m, M)[:8]))
     res["msm_batch_small"] = {"msms": 8, "terms_each": m, "ms": small["host_horner"], "fused_ms": small["fused"],
                               "same_result_as_fused_batch": same_small}
+    res["verifier_msms"] = verifier_msm_rows(ob)
     # f1 with fixed bases: the same batch, each term referencing a row of a 4096-row base table
     #   (created once, rows precomputed as 2^(8w) P: one bucket set per MSM, no window Horner)
     rows = 4096
@@ -379,8 +438,8 @@ def main():
     # ---- KZG decider (config 3): accumulators per GPU (N > 1: rank r holds global accumulators
     #      [r dn, (r + 1) dn) and the first failing global index comes from one MIN all-reduce)
     dn = args.decider_n
-    g2, sg2, accs = ob.gen_decider_case(16, seed=ob.SEED_TRAPDOOR)
-    accs = (accs * ((dn + 15) // 16))[:dn]
+    # dn distinct valid accumulators per rank (rank r: the seeded t_i for i in [r dn, (r + 1) dn))
+    g2, sg2, accs = ob.gen_decider_case(dn, seed=ob.SEED_TRAPDOOR, start=rank * dn)
     from svgpu import encoding as enc
     L = torch.from_numpy(enc.bases_array([a[0] for a in accs]).view(np.int64)).to(dev)
     R = torch.from_numpy(enc.bases_array([a[1] for a in accs]).view(np.int64)).to(dev)

@@ -1118,13 +1118,14 @@ SEED_BASES = 0xBA5E5
 SEED_TRAPDOOR = 0xD3C1DE
 
 
-def gen_decider_case(n: int, seed: int = SEED_TRAPDOOR, bad: Sequence[int] = ()):
-    """dk = (G1, G2, s G2); acc_i = (s t_i G1, t_i G1); lhs_k += G1 for k in `bad`."""
+def gen_decider_case(n: int, seed: int = SEED_TRAPDOOR, bad: Sequence[int] = (), start: int = 0):
+    """dk = (G1, G2, s G2); acc_i = (s t_i G1, t_i G1) with t_i the seeded scalar start + i (every
+    accumulator distinct); lhs_k += G1 for k in `bad`."""
     s = gen_scalar(seed, 0)
     s_g2 = g2_mul(G2_GEN, s)
     accs = []
     for i in range(n):
-        t = gen_scalar(seed, 1 + i)
+        t = gen_scalar(seed, 1 + start + i)
         rhs = g1_mul(G1_GEN, t)
         lhs = g1_mul(G1_GEN, s * t % R)
         if i in bad:

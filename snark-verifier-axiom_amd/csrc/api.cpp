@@ -98,7 +98,15 @@ int for_each_device(int ndev, Fn fn) {
 struct Staging {
   WsLease lease;
   std::vector<char*> d;
+  bool pending = false;  // async copies queued since the last sync (they may read caller memory)
   explicit Staging(int device) : lease(device, nullptr) {}
+  Staging(const Staging&) = delete;
+  Staging& operator=(const Staging&) = delete;
+  // An early error return must not hand the workspace back to the pool (or free the host memory
+  // a queued copy reads) while copies are still in flight.
+  ~Staging() {
+    if (pending && lease.ok()) (void)hipStreamSynchronize(lease.get()->stream);
+  }
   int init(std::initializer_list<size_t> sizes) {
     if (!lease.ok()) return SV_ERR_DEVICE;
     size_t tot = 0;
@@ -116,19 +124,23 @@ struct Staging {
     return reinterpret_cast<T*>(d[i]);
   }
   int put(int i, const void* h, size_t bytes) {
+    pending = true;
     if (bytes) SV_HIP(hipMemcpyAsync(d[i], h, bytes, hipMemcpyHostToDevice, lease.get()->stream));
     return SV_OK;
   }
   int put_at(int i, size_t offset, const void* h, size_t bytes) {
+    pending = true;
     if (bytes) SV_HIP(hipMemcpyAsync(d[i] + offset, h, bytes, hipMemcpyHostToDevice, lease.get()->stream));
     return SV_OK;
   }
   int get(void* h, int i, size_t bytes) {
+    pending = true;
     if (bytes) SV_HIP(hipMemcpyAsync(h, d[i], bytes, hipMemcpyDeviceToHost, lease.get()->stream));
     return SV_OK;
   }
   int sync() {
     SV_HIP(hipStreamSynchronize(lease.get()->stream));
+    pending = false;
     return SV_OK;
   }
 };
@@ -476,12 +488,20 @@ int sv_bn254_kzg_accumulate(const sv_g1_affine* lhs, const sv_g1_affine* rhs, si
     Xyzz ab[2];
     SV_TRY(msm_batch_windows_host(sg.at(0), sg.at(1), sg.at<const uint64_t>(2), 2, n, SV_MONTGOMERY, form, dev,
                                   sg.lease.get()->stream, ab));
+    sg.pending = false;  // msm_batch_windows_host synchronised the stream
     affine_out(ab[0], form, out_lhs);
     affine_out(ab[1], form, out_rhs);
     return SV_OK;
   }
   Staging sg(dev);
-  SV_TRY(sg.init({n * sizeof(sv_g1_affine), n * sizeof(sv_g1_affine), n * sizeof(sv_fe), sizeof(sv_fe)}));  // the lhs and rhs MSMs share the scalars and are independent: run them concurrently (each call
+  SV_TRY(sg.init({n * sizeof(sv_g1_affine), n * sizeof(sv_g1_affine), n * sizeof(sv_fe), sizeof(sv_fe)}));
+  SV_TRY(sg.put(0, lhs, n * sizeof(sv_g1_affine)));
+  SV_TRY(sg.put(1, rhs, n * sizeof(sv_g1_affine)));
+  SV_TRY(sg.put(3, r, sizeof(sv_fe)));
+  SV_TRY(sg.sync());
+  SV_TRY(powers_device(sg.at(3), form, n, form, sg.at(2), sg.lease.get()->stream));
+  SV_TRY(sg.sync());
+  // the lhs and rhs MSMs share the scalars and are independent: run them concurrently (each call
   // leases its own stream + workspace), one on the caller and one on a pool worker
   Xyzz ab[2];
   int rc2[2] = {SV_OK, SV_OK};
@@ -599,11 +619,14 @@ int sv_bn254_g1_msm_batch(const sv_g1_affine* bases, const sv_fe* scalars, const
   const uint64_t base = offsets[0], total = offsets[count] - base;
   std::vector<uint64_t> off(offsets, offsets + count + 1);
   for (auto& o : off) o -= base;
-  // The batch kernel costs about one Horner chain (~2 ms) whatever the batch size; the single-MSM
-  // pipeline finishes its (host-side) Horner in ~0.35 ms per MSM.  Tiny batches go sequential.
+  // The fused batch kernel costs about one Horner chain (~0.65 ms) whatever the batch size, so in a
+  // tiny batch (at most SVGPU_BATCH_SEQ_MAX MSMs) the MSMs above kSmallMsmTerms terms go through the
+  // single-MSM pipeline one by one.  MSMs of at most kSmallMsmTerms terms stay in the batch: a batch
+  // of only such MSMs passes no id map, so msm_batch_device can take its small-batch route (window
+  // sums on the device, one host Horner per MSM: 0.17-0.20 ms for 1-16 MSMs of 64 terms).
   size_t seq_max = 4;
   if (const char* e = getenv("SVGPU_BATCH_SEQ_MAX")) seq_max = strtoull(e, nullptr, 10);
-  if (count <= seq_max) big_limit = 0;
+  if (count <= seq_max) big_limit = std::min(big_limit, kSmallMsmTerms);
   std::vector<uint32_t> small_ids, big_ids;
   size_t max_small = 0;
   for (size_t k = 0; k < count; k++) {
@@ -624,8 +647,10 @@ int sv_bn254_g1_msm_batch(const sv_g1_affine* bases, const sv_fe* scalars, const
   SV_TRY(sg.put(3, small_ids.data(), small_ids.size() * sizeof(uint32_t)));
   SV_TRY(sg.sync());
   if (!small_ids.empty()) {
-    SV_TRY(msm_batch_device(sg.at(0), sg.at(1), sg.at<const uint64_t>(2), sg.at<const uint32_t>(3),
-                            small_ids.size(), max_small, form, dev, nullptr, sg.at(4)));
+    // every MSM small: no id map (the ids would be the identity), which the small-batch route needs
+    const uint32_t* ids = big_ids.empty() ? nullptr : sg.at<const uint32_t>(3);
+    SV_TRY(msm_batch_device(sg.at(0), sg.at(1), sg.at<const uint64_t>(2), ids, small_ids.size(), max_small, form, dev,
+                            nullptr, sg.at(4)));
     SV_TRY(sg.get(out, 4, count * sizeof(sv_g1_affine)));
     SV_TRY(sg.sync());
   }

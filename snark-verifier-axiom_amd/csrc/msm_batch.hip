@@ -1020,10 +1020,7 @@ __global__ void __launch_bounds__(kThreads) k_msm_batch_fixed(const G1Aff* __res
 
 }  // namespace
 
-static std::atomic<uint64_t> g_fused_redone{0};
-int msm_batch_windows_host(const void* d_bases, const void* d_scalars, const uint64_t* d_offsets, size_t count,
-                           size_t max_terms, int scalar_form, int base_form, int device, hipStream_t stream,
-                           host::Xyzz* out);  // fused launches redone by the two-kernel path
+static std::atomic<uint64_t> g_fused_redone{0};  // fused launches redone by the two-kernel path
 
 int msm_batch_window_bits(size_t max_terms) {
   if (const char* e = getenv("SVGPU_BATCH_WINDOW_BITS")) {
@@ -1065,8 +1062,11 @@ static int msm_batch_small_host(const void* d_bases, const void* d_scalars, cons
     memcpy(&h[8 * k], x.l, 32);
     memcpy(&h[8 * k + 4], y.l, 32);
   }
+  // on the caller's stream (no null-stream implicit sync); this route is synchronous for the host
+  // anyway (msm_batch_windows_host waited for the window sums), so wait for the copy of `h`
   SV_HIP(hipSetDevice(device));
-  SV_HIP(hipMemcpy(d_out, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+  SV_HIP(hipMemcpyAsync(d_out, h.data(), h.size() * 8, hipMemcpyHostToDevice, stream));
+  SV_HIP(hipStreamSynchronize(stream));
   return SV_OK;
 }
 

@@ -60,17 +60,23 @@ def allgather_partials(partial: Jacobian, group=None) -> list:
     return [_unpack(host[96 * r:96 * (r + 1)]) for r in range(world)]
 
 
-def sharded_msm(partial_fn: Callable[[], Jacobian], group=None) -> Point:
-    """Run this rank's shard (``partial_fn``), exchange partials, fold in rank order."""
-    partial = partial_fn()
+IDENTITY: Jacobian = (1, 1, 0)
+
+
+def sharded_msm(partial_fn: Callable[[], Jacobian], group=None, local_terms: Optional[int] = None) -> Point:
+    """Run this rank's shard (``partial_fn``), exchange partials, fold in rank order.  A rank whose
+    shard is empty (``local_terms == 0``: more ranks than points, the tail of an uneven split)
+    contributes the identity without calling ``partial_fn`` -- the library rejects an empty MSM --
+    and still takes part in the all-gather."""
+    partial = IDENTITY if local_terms == 0 else partial_fn()
     return fold_partials(allgather_partials(partial, group))
 
 
 def sharded_msm_device(bases: torch.Tensor, scalars: torch.Tensor, form: int, group=None) -> Point:
-    """``bases``/``scalars`` are THIS rank's shard, resident in HBM."""
+    """``bases``/``scalars`` are THIS rank's shard, resident in HBM (possibly empty)."""
     from .device import msm_partial
 
-    return sharded_msm(lambda: msm_partial(bases, scalars, form), group)
+    return sharded_msm(lambda: msm_partial(bases, scalars, form), group, local_terms=int(bases.shape[0]))
 
 
 def combine_first_fail(local_first_fail: int, shard_offset: int, group=None) -> int:
@@ -92,5 +98,12 @@ def sharded_decide_device(g2, s_g2, lhs: torch.Tensor, rhs: torch.Tensor, shard_
     (decider.rs:70-80)."""
     from .device import decide
 
-    local, _, _ = decide(g2, s_g2, lhs, rhs, form)
+    return sharded_decide(lambda: decide(g2, s_g2, lhs, rhs, form)[0], int(lhs.shape[0]), shard_offset, group)
+
+
+def sharded_decide(local_fn: Callable[[], int], local_count: int, shard_offset: int, group=None) -> int:
+    """The exchange of ``sharded_decide_device`` around any per-rank decider ``local_fn`` (local first
+    failing index or -1).  An empty shard passes without a call (the library rejects an empty batch)
+    and still joins the all-reduce."""
+    local = -1 if local_count == 0 else local_fn()
     return combine_first_fail(local, shard_offset, group)

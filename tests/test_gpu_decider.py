@@ -48,10 +48,8 @@ def test_256_accumulators_vs_cpp(gpu, oracle_cpp):
     import svgpu
     from svgpu import encoding as enc
     n = 256
-    g2, sg2, accs = b.gen_decider_case(16, seed=0xD3C1DE)
-    accs = (accs * (n // 16))[:n]
     bad = 201
-    accs[bad] = (b.g1_add(accs[bad][0], b.G1_GEN), accs[bad][1])
+    g2, sg2, accs = b.gen_decider_case(n, seed=0xD3C1DE, bad=[bad])  # 256 distinct accumulators
     L = enc.bases_array([a[0] for a in accs])
     R = enc.bases_array([a[1] for a in accs])
     dk = svgpu.KzgDecidingKey(b.G1_GEN, g2, sg2)
@@ -266,3 +264,53 @@ def test_decider_verdict_copy_path(gpu, oracle_cpp, monkeypatch):
                                    L, R, threads=0, want_gt=False)
     assert got["1"] == got["0"] and got["1"][0] == eff == 3
     assert [i for i, v in enumerate(got["1"][1]) if not v] == [3, 8]
+
+
+@pytest.mark.parametrize("n,small_off", [(257, False), (1000, False), (64, True), (5, True)])
+def test_accumulate_pipeline_route_vs_cpp(gpu, oracle_cpp, monkeypatch, n, small_off):
+    """sv_bn254_kzg_accumulate on the single-MSM pipeline route -- more accumulators than the
+    small-MSM window path takes (n > 256), or that path switched off (SVGPU_SMALL_MSM=0) -- against
+    the C++ oracle's r^i MSMs (accumulation.rs:177-192, loader.rs:71-78).  Regression for ADVICE r05
+    (high): the route had lost its input uploads and the r^i powers."""
+    import ctypes
+    import svgpu
+    from svgpu import _lib, encoding as enc
+    if small_off:
+        monkeypatch.setenv("SVGPU_SMALL_MSM", "0")
+    L = oracle_cpp.gen_bases(0xACC0 + n, n)
+    R_ = oracle_cpp.gen_bases(0xACC1 + n, n)
+    r = b.gen_scalar(0xACC2, n)
+    el, er = oracle_cpp.accumulate(L, R_, enc.ints_to_limbs([r])[0])
+    # twice: the second call reuses a pooled workspace that still holds the first call's data
+    for rr in (r, (r * 3 + 1) % b.R):
+        ol, orr = _lib.sv_g1_affine(), _lib.sv_g1_affine()
+        _lib.check(_lib.lib.sv_bn254_kzg_accumulate(L.ctypes.data, R_.ctypes.data, n, ctypes.byref(enc.fe_struct(rr)),
+                                                    svgpu.SV_CANONICAL, 0, ctypes.byref(ol), ctypes.byref(orr)),
+                   "sv_bn254_kzg_accumulate")
+        if rr == r:
+            assert enc.g1_from_struct(ol) == enc.g1_from_limbs(el)
+            assert enc.g1_from_struct(orr) == enc.g1_from_limbs(er)
+        else:
+            e2l, e2r = oracle_cpp.accumulate(L, R_, enc.ints_to_limbs([rr])[0])
+            assert (enc.g1_from_struct(ol), enc.g1_from_struct(orr)) == (enc.g1_from_limbs(e2l), enc.g1_from_limbs(e2r))
+
+
+def test_create_proof_300_accumulators_vs_oracle(gpu, oracle_cpp):
+    """create_proof over 300 accumulators (the pipeline route for its r^i MSMs): r from the
+    transcript restatement, the MSMs from the C++ oracle."""
+    import svgpu
+    from oracle import poseidon as op
+    from svgpu import encoding as enc
+    n = 300
+    L = oracle_cpp.gen_bases(0xC300, n)
+    R_ = oracle_cpp.gen_bases(0xC301, n)
+    accs = [(enc.g1_from_limbs(L[i]), enc.g1_from_limbs(R_[i])) for i in range(n)]
+    sp = op.Sponge(3)
+    for a in accs:
+        op.transcript_common_ec_point(sp, a[0])
+        op.transcript_common_ec_point(sp, a[1])
+    r = sp.squeeze()
+    out = svgpu.KzgAs.create_proof([svgpu.KzgAccumulator(*a) for a in accs])
+    assert svgpu.KzgAs.last_challenge == r
+    el, er = oracle_cpp.accumulate(L, R_, enc.ints_to_limbs([r])[0])
+    assert (out.lhs, out.rhs) == (enc.g1_from_limbs(el), enc.g1_from_limbs(er))

@@ -79,9 +79,17 @@ def test_big_msms_route_to_single_pipeline(gpu, oracle_cpp, monkeypatch):
     assert svgpu.msm_batch_arrays(B, S, off) == _expected(oracle_cpp, B, S, off)
 
 
-def test_tiny_batch_sequential_route(gpu, oracle_cpp):
+@pytest.mark.parametrize("sizes", [[64, 64], [30], [12, 40, 7, 256], [300, 64], [64, 1000, 3], [257]])
+@pytest.mark.parametrize("host_max", [None, "0"])
+def test_tiny_batch_sequential_route(gpu, oracle_cpp, monkeypatch, sizes, host_max):
+    """Host-array batches of at most SVGPU_BATCH_SEQ_MAX (4) MSMs: the MSMs of at most 256 terms
+    stay in the batch (all-small batches take the small-batch host-Horner route, no id map; mixed
+    ones the id-mapped batch kernel), the longer ones run through the single-MSM pipeline.  The
+    config-5 shape (two 64-term MSMs) and a proof's few tens-term MSMs (bdfg21.rs:75-78) included."""
     import svgpu
-    B, S, off = _ragged(oracle_cpp, [64, 64], 9000)  # config-5 shape: two 64-term MSMs
+    if host_max is not None:
+        monkeypatch.setenv("SVGPU_BATCH_HOST_MAX", host_max)
+    B, S, off = _ragged(oracle_cpp, sizes, 9000 + len(sizes))
     assert svgpu.msm_batch_arrays(B, S, off) == _expected(oracle_cpp, B, S, off)
 
 

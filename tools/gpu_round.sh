@@ -20,6 +20,8 @@ run prof/trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpuru
 run prof/trace_extras 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace_extras -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
 run prof/pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof/pmc_fetch -o run -- python3 $B
 run prof/pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof/pmc_write -o run -- python3 $B
+# the calibration binary is not uploaded (.gpurunignore): build it on the box
+[ -x tools/calib_fetch ] || run build_calib 300 /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 tools/calib_fetch.hip -o tools/calib_fetch
 run prof/pmc_calib 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof/pmc_calib -o run -- ./tools/calib_fetch
 run prof/sq_valu 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 SQ_ACTIVE_INST_VALU SQ_INSTS_SALU --output-format csv -d gpurun_out/prof/sq_valu -o run -- python3 $B
 run prof/sq_wait 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM --output-format csv -d gpurun_out/prof/sq_wait -o run -- python3 $B

@@ -1,8 +1,10 @@
 """Summarise a rocprofv3 run (tools/profile_*.sh) into profiles/: kernel-stats table + PMC HBM bytes.
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  gfx950 correction (MI355X_MICROARCH.md, HBM):
-FETCH_SIZE reads exactly half the bytes of wide (16 B/lane) coalesced streaming reads; other access
-widths are uncalibrated, so both the raw and the x2-corrected read figures are recorded.
+FETCH_SIZE reads exactly half the bytes of wide (16 B/lane) coalesced streaming reads.  That x2 is
+applied only to kernels that stream; k_accumulate gathers 64-B points at random and gets the factor
+calibrated on that pattern (tools/calib_fetch.hip, ~1.05 from a 64 MiB table) -- the same factor
+profiles/pmc_accumulate.json and bench.py's roofline.traffic use.  Each row names its factor.
 usage: python3 tools/summarize_profile.py gpurun_out/prof profiles r02
 """
 import csv
@@ -40,13 +42,6 @@ for counter, sub in (("FETCH_SIZE", "pmc_fetch"), ("WRITE_SIZE", "pmc_write")):
     for r in csv.DictReader(open(os.path.join(src, sub, "run_counter_collection.csv"))):
         acc[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     pmc[counter] = {k: sum(v) / len(v) for k, v in acc.items()}
-lines += ["", "## HBM traffic per launch (PMC, separate passes)", "",
-          "| kernel | FETCH_SIZE KiB (raw) | reads x2 corrected MB | WRITE_SIZE KiB | MB total (corrected) |",
-          "|---|---|---|---|---|"]
-for k in sorted(pmc["FETCH_SIZE"], key=lambda k: -pmc["FETCH_SIZE"][k]):
-    f = pmc["FETCH_SIZE"][k]
-    w = pmc["WRITE_SIZE"].get(k, 0.0)
-    lines.append("| %s | %.0f | %.1f | %.0f | %.1f |" % (k, f, 2 * f * 1024 / 1e6, w, (2 * f + w) * 1024 / 1e6))
 # FETCH_SIZE calibration (tools/calib_fetch.hip): known bytes / FETCH_SIZE bytes per kernel dispatch
 calib = {}
 cal_csv = os.path.join(src, "pmc_calib", "run_counter_collection.csv")
@@ -63,6 +58,28 @@ if os.path.exists(cal_csv):
               "| pattern | FETCH_SIZE KiB | known MB | factor (known / FETCH_SIZE) |", "|---|---|---|---|"]
     for k, v in calib.items():
         lines.append("| %s | %.0f | %.1f | %.3f |" % (k, v["fetch_kib"], v["known_bytes"] / 1e6, v["factor"] or 0))
+GATHER_KERNELS = ("k_accumulate",)  # random 64-B point gathers (bucket entries in sorted order)
+
+
+def read_factor(kernel):
+    """(factor, basis) for FETCH_SIZE of one kernel: the gather calibration for the gathering
+    kernels, the guide's streaming x2 (or its calibrated value) for the rest."""
+    if kernel.startswith(GATHER_KERNELS):
+        g = calib.get("gather64_64MiB", {}).get("factor")
+        return (g, "gather64 calibrated") if g else (1.05, "gather64 (round-2 calibration)")
+    st = calib.get("stream16", {}).get("factor")
+    return (st, "stream16 calibrated") if st else (2.0, "streaming x2 (guide)")
+
+
+lines += ["", "## HBM traffic per launch (PMC, separate passes)", "",
+          "| kernel | FETCH_SIZE KiB (raw) | read factor | basis | reads MB | WRITE_SIZE KiB | MB total |",
+          "|---|---|---|---|---|---|---|"]
+for k in sorted(pmc["FETCH_SIZE"], key=lambda k: -pmc["FETCH_SIZE"][k]):
+    f = pmc["FETCH_SIZE"][k]
+    w = pmc["WRITE_SIZE"].get(k, 0.0)
+    fac, basis = read_factor(k)
+    lines.append("| %s | %.0f | %.3f | %s | %.1f | %.0f | %.1f |" % (k, f, fac, basis, fac * f * 1024 / 1e6, w,
+                                                                   (fac * f + w) * 1024 / 1e6))
 # SQ instruction / cycle counters (round 5: sq_valu, sq_wait passes), per dispatch, for the two
 # dominant kernels; per-wave figures divide by SQ_WAVES
 sq = {}
@@ -91,13 +108,13 @@ acc_f = pmc["FETCH_SIZE"].get(acc_key) if acc_key else None
 acc_w = pmc["WRITE_SIZE"].get(acc_key) if acc_key else None
 if acc_f is not None:
     g = calib.get("gather64_64MiB", {}).get("factor")
-    factor = g if g else 2.0
+    factor = read_factor(acc_key)[0]
     json.dump({"kernel": "k_accumulate", "source": f"profiles/{tag}_kernel_stats.md",
                "fetch_kib_raw": acc_f, "write_kib": acc_w, "read_factor": factor,
                "hbm_bytes_per_launch": (factor * acc_f + (acc_w or 0)) * 1024,
                "correction": "reads scaled by the factor calibrated on k_accumulate's own access pattern "
                              "(random 64-B gathers from a 64 MiB table, tools/calib_fetch.hip) -- the "
                              "MI355X_MICROARCH.md HBM note calibrates only 16-B streaming reads (x2)"
-                             if g else "reads doubled per MI355X_MICROARCH.md HBM note (calibration missing)"},
+                             if g else "reads x1.05, the round-2 gather calibration (no calibration pass in this run)"},
               open(os.path.join(dst, "pmc_accumulate.json"), "w"), indent=1)
 print("\n".join(lines))

@@ -179,10 +179,14 @@ pub fn last_error() -> String {
     }
 }
 
-/// Smallest MSM routed to the GPU (SVGPU_MIN_MSM, default 64): below it the launch dominates.
+/// Smallest MSM routed to the GPU (SVGPU_MIN_MSM, default 2).  Measured on the MI355X box
+/// (bench.py `verifier_msms.crossover`, profiles/r06_verifier_msms.json): one library call
+/// (sv_bn254_g1_msm_refs: gather + copy + the small-MSM window path + host Horner) takes
+/// 0.13-0.16 ms from 1 to 64 terms, the reference's naive CPU sum ~0.097 ms per term, so the GPU
+/// wins from 2 terms -- a verifier's tens-term MSMs (bdfg21.rs:75-78) go to the GPU.
 pub fn min_msm() -> usize {
     static INIT: Once = Once::new();
-    static MIN: AtomicUsize = AtomicUsize::new(64);
+    static MIN: AtomicUsize = AtomicUsize::new(2);
     // call_once's completion happens-before every later return from it, so a relaxed load sees it
     INIT.call_once(|| {
         if let Some(v) = std::env::var("SVGPU_MIN_MSM").ok().and_then(|v| v.parse::<usize>().ok()) {

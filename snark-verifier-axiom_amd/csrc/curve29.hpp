@@ -62,6 +62,36 @@ SV29_HD Xyzz madd(const Xyzz& p, const F& x2, const F& y2, bool neg) {
 }
 SV29_HD Xyzz madd(const Xyzz& p, const F& x2, const F& y2) { return madd(p, x2, y2, false); }
 
+// Round 6: the bucket chain's two halves of madd for a loop that never lets its state be the
+// identity (k_accumulate, SVGPU_ACC_LOOP=1): a segment starts with its first point (start) in the
+// loop's divergent segment-end block, and the per-entry step (madd_live) has no identity test and
+// no identity-valued exit -- the merges those needed cost ~100 VALU instructions per entry (register
+// copies, 36 zeroing moves, the identity branch).  P + (-P) sets `cancel` and leaves a meaningless
+// state: the caller marks the chain empty and restarts it with its next point.
+SV29_HD Xyzz start(const F& x2, const F& y2, bool neg) { return {x2, neg ? sub<2>(zero(), y2) : y2, one(), one()}; }
+SV29_HD Xyzz madd_live(const Xyzz& p, const F& x2, const F& y2, bool neg, bool& cancel) {
+  F Pd = mul_sub<8>(x2, p.ZZ, p.X);                  // U2 - X + 8p, fused: < 10p (state X < 8p)
+  F Rd = sub_sgn<4>(mul(y2, p.ZZZ), neg, p.Y);       // +-S2 - Y + 4p: < 6p
+  F X = p.X, Y = p.Y, ZZ = p.ZZ, ZZZ = p.ZZZ;
+  bool dbl = false;
+  if (is_zero_mod_p_10p(Pd)) {
+    if (!is_zero_mod_p_6p(Rd)) {
+      cancel = true;  // P + (-P): the caller restarts the chain (the products below run on as garbage)
+    } else {
+      const F x2s = sqr(x2), ys = neg ? sub<2>(zero(), y2) : y2;
+      Pd = add(ys, ys);               // < 4p
+      Rd = add(add(x2s, x2s), x2s);   // < 6p
+      X = x2, Y = ys, ZZ = one(), ZZZ = one();
+      dbl = true;
+    }
+  }
+  const F PP = sqr(Pd), PPP = mul(Pd, PP), Q = mul(X, PP);  // < 2p
+  // X3 = Rd^2 [- PPP] - 2Q + 6p in the square's high columns: in (0, 8p)
+  const F X3 = sqr_sub2c<6>(Rd, dbl ? zero() : PPP, Q);
+  const F Y3 = mul_sum2(Rd, sub<8>(Q, X3), Y, sub<2>(zero(), PPP));
+  return {X3, Y3, mul(ZZ, PP), mul(ZZZ, PPP)};
+}
+
 // p + q, both XYZZ states (bounds as above; either may be the identity).  add-2008-s; the
 // doubling case (p = q) runs through the same products as in madd: dbl-2008-s-1's U = 2Y, M = 3X²,
 // S = X V, ZZ3 = V ZZ, ZZZ3 = W ZZZ are the addition's Pd, Rd, Q, ZZ3, ZZZ3 with U1 = X, S1 = Y and

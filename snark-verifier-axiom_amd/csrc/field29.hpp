@@ -224,7 +224,70 @@ SV29_HD F29<M> mul_sum3(const F29<M>& a0, const F29<M>& b0, const F29<M>& a1, co
   t.v[L - 1] = (uint32_t)acc;
   return t;
 }
+// Round 6: a product with a normalized subtraction fused into its high columns.  The caller's
+// per-limb addends D_i (each in [0, 2^32)) go into column L + i before the column's carry-out, so
+// the result is a b / R' + sum D_i 2^(29 i), with the top limb masked to 29 bits: multiples of 2^261
+// vanish.  A subtraction a b / R' + K p - c becomes D_i = K p_i + 2^29 - [i > 0] - c_i (the
+// borrow of 2^29 per limb sums to exactly 2^261), which saves the separate pass's per-limb add,
+// arithmetic shift and mask.  The caller guarantees that the true value lies in [0, 2^261).
+template <class M>
+SV29_HD F29<M> mul_add_hi(const F29<M>& a, const F29<M>& b, const uint32_t D[L]) {
+  uint32_t m[L];
+  F29<M> t;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * L - 1; k++) {
+    if (k >= L) acc += D[k - L];
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < L) acc = mad(a.v[i], b.v[j], acc);
+    }
+    SV29_REDUCE_COLUMN(k)
+  }
+  t.v[L - 1] = ((uint32_t)acc + D[L - 1]) & MASK;
+  return t;
+}
+template <class M>
+SV29_HD F29<M> sqr_add_hi(const F29<M>& a, const uint32_t D[L]) {
+  uint32_t m[L], a2[L];
+  F29<M> t;
+#pragma unroll
+  for (int i = 0; i < L; i++) a2[i] = a.v[i] << 1;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * L - 1; k++) {
+    if (k >= L) acc += D[k - L];
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+      const int j = k - i;
+      if (j > i && j < L) acc = mad(a.v[i], a2[j], acc);
+    }
+    if ((k & 1) == 0 && k / 2 < L) acc = mad(a.v[k / 2], a.v[k / 2], acc);
+    SV29_REDUCE_COLUMN(k)
+  }
+  t.v[L - 1] = ((uint32_t)acc + D[L - 1]) & MASK;
+  return t;
+}
 #undef SV29_REDUCE_COLUMN
+
+// a b / R' + K p - c (c normalized, below K p; the result below 2p + K p): mul_add_hi
+template <int K, class M>
+SV29_HD F29<M> mul_sub(const F29<M>& a, const F29<M>& b, const F29<M>& c) {
+  uint32_t D[L];
+#pragma unroll
+  for (int i = 0; i < L; i++) D[i] = (M::kp(K, i) + (1u << 29) - (i > 0 ? 1u : 0u)) - c.v[i];
+  return mul_add_hi(a, b, D);
+}
+// a^2 / R' + K p - b - 2 c (b, c normalized, b + 2c below K p; below 2p + K p): the XYZZ
+// addition's X3 = R^2 - PPP - 2Q + 6p in the square's high columns
+template <int K, class M>
+SV29_HD F29<M> sqr_sub2c(const F29<M>& a, const F29<M>& b, const F29<M>& c) {
+  uint32_t D[L];
+#pragma unroll
+  for (int i = 0; i < L; i++) D[i] = (M::kp(K, i) + (3u << 29) - (i > 0 ? 3u : 0u)) - (b.v[i] + (c.v[i] << 1));
+  return sqr_add_hi(a, D);
+}
 
 // a b / R' mod p like mul (inputs below 12p -> output below 2p), scheduled for the latency of ONE
 // wave (the decider's lane products, round 5): the 81 partial products go to 17 separate 64-bit

@@ -89,6 +89,15 @@ __device__ __forceinline__ G1Aff load_vpoint(const G1Aff* __restrict__ bases, co
   return r;
 }
 
+// all-zero words: the identity in both stored forms (ZZ = 0)
+__device__ __forceinline__ G1Xyzz zero_xyzz() {
+  G1Xyzz r;
+  uint32_t* d = reinterpret_cast<uint32_t*>(&r);
+#pragma unroll
+  for (int k = 0; k < 32; k++) d[k] = 0;
+  return r;
+}
+
 __device__ __forceinline__ G1Xyzz load_xyzz(const G1Xyzz* __restrict__ a, uint32_t i) {
   const uint4* p = reinterpret_cast<const uint4*>(a + i);
   G1Xyzz r;
@@ -904,7 +913,11 @@ struct AccChain<true> {
 #ifndef SV_ACC29_MIN_BLOCKS
 #define SV_ACC29_MIN_BLOCKS 4
 #endif
-template <bool ADD, bool R29, int PF = SV_ACC_PREFETCH>
+// NL (round 6, the 29-bit chain only; SVGPU_ACC_LOOP=0 keeps the round-5 loop): the chain's state
+// is never the identity -- a lane whose chain is empty (segment start, or after P + (-P)) takes its
+// next point as the state in the loop's divergent segment-end block and skips that entry's madd, so
+// the per-entry step is r29::madd_live with no identity test or identity-valued merge.
+template <bool ADD, bool R29, int PF = SV_ACC_PREFETCH, bool NL = R29>
 __global__ void __launch_bounds__(kBlock, R29 ? SV_ACC29_MIN_BLOCKS : SV_ACC_MIN_BLOCKS) k_accumulate(
     const G1Aff* __restrict__ bases, const uint32_t* __restrict__ ent, const uint32_t* __restrict__ gst,
     const uint32_t* __restrict__ tstart, uint32_t nbt, uint32_t K, uint32_t T,
@@ -932,13 +945,62 @@ __global__ void __launch_bounds__(kBlock, R29 ? SV_ACC29_MIN_BLOCKS : SV_ACC_MIN
     // ADD (host-fed pieces after the first): a segment that starts its bucket -- the owner piece --
     // starts from the sum the earlier pieces left in bsum (identity-initialised) instead of the
     // identity, so every later join (in block, k_fixup) and store carries it: no extra addition
+    bool empty = true;  // NL: the chain holds no point yet (acc is not read)
     if constexpr (ADD) {
-      if (s0 == gs) acc = A::in(load_xyzz(bsum, g));
+      if (s0 == gs) {
+        acc = A::in(load_xyzz(bsum, g));
+        if constexpr (NL) empty = r29::is_zero(acc.ZZ);
+      }
     }
     uint32_t vnext = 0;
     if constexpr (PF >= 1) vnext = ent[s0];
     G1Aff pnext;
     if constexpr (PF >= 2) pnext = load_vpoint(bases, phix, vnext & 0x7fffffffu, nsplit, phi64);
+    if constexpr (NL) {
+      static_assert(R29 && PF == 1, "the restructured loop is the 29-bit chain's");
+      for (uint32_t e = s0; e < e_end; e++) {
+        // the entry's point first: a segment starting here starts from it
+        const uint32_t v = vnext;
+        if (e + 1 < e_end) vnext = ent[e + 1];
+        const G1Aff p = load_vpoint(bases, phix, v & 0x7fffffffu, nsplit, phi64);
+        const bool live = !p.is_identity(), neg = (v & 0x80000000u) != 0;
+        const r29::F x = r29::from_words(p.x.v), y = r29::from_words(p.y.v);  // the table's x R' words
+        bool fresh = false;
+        if (e >= ge || empty) {  // divergent: a segment ends here, or the chain is empty
+          if (e >= ge) {  // segment [seg_start, ge) of bucket g ends inside this chunk
+            const G1Xyzz sum = empty ? zero_xyzz() : A::out(acc);
+            if (seg_start == gs) {
+              store_xyzz(bsum, g, sum);
+            } else {  // head piece of a bucket owned by an earlier thread
+              if (join_in_block(gs, ge, K)) shead[threadIdx.x] = sum;
+              else store_xyzz(pfirst, t, sum);
+            }
+            first = false;
+            do {
+              g++;
+              gs = ge;
+              ge = gst[g + 1];
+            } while (ge <= e);
+            seg_start = e;
+            empty = true;
+            if constexpr (ADD) {
+              acc = A::in(load_xyzz(bsum, g));
+              empty = r29::is_zero(acc.ZZ);
+            }
+          }
+          if (empty && live) {
+            acc = r29::start(x, y, neg);
+            empty = false;
+            fresh = true;
+          }
+        }
+        if (live && !fresh) {
+          bool cancel = false;
+          acc = r29::madd_live(acc, x, y, neg, cancel);
+          if (cancel) empty = true;
+        }
+      }
+    } else
     for (uint32_t e = s0; e < e_end; e++) {
       if (e >= ge) {  // segment [seg_start, ge) of bucket g ends inside this chunk
         const G1Xyzz sum = A::out(acc);
@@ -978,7 +1040,8 @@ __global__ void __launch_bounds__(kBlock, R29 ? SV_ACC29_MIN_BLOCKS : SV_ACC_MIN
       }
       if (!p.is_identity()) acc = A::madd(acc, p, (v & 0x80000000u) != 0);
     }
-    sum = A::out(acc);
+    if constexpr (NL) sum = empty ? zero_xyzz() : A::out(acc);
+    else sum = A::out(acc);
     if (seg_start == gs && e_end == ge) {
       store_xyzz(bsum, g, sum);
     } else if (seg_start != gs) {  // first segment, bucket started earlier (it may also go on later)
@@ -1769,8 +1832,11 @@ static int msm_acc(const MsmPlan& p, const MsmScratch& w, const SortOut& so, con
     phix = nullptr;
     nsplit = ~0u;
   }
-  auto kern = add_into ? (r29 ? k_accumulate<true, true> : k_accumulate<true, false>)
-                       : (r29 ? k_accumulate<false, true> : k_accumulate<false, false>);
+  const bool old_loop = getenv("SVGPU_ACC_LOOP") && atoi(getenv("SVGPU_ACC_LOOP")) == 0;  // read per call
+  auto kern = add_into ? (r29 ? (old_loop ? k_accumulate<true, true, SV_ACC_PREFETCH, false> : k_accumulate<true, true>)
+                              : k_accumulate<true, false>)
+                       : (r29 ? (old_loop ? k_accumulate<false, true, SV_ACC_PREFETCH, false> : k_accumulate<false, true>)
+                              : k_accumulate<false, false>);
   hipLaunchKernelGGL(kern, dim3(cdiv(so.T, kBlock)), dim3(kBlock), 0, st, bases, so.ent, so.gst, so.tstart, nbt,
                      so.K, so.T, bsum, w.pfirst, w.plast, w.multi, w.nmulti, w.heavy, w.nheavy, phix, nsplit,
                      p.phi64);

@@ -55,13 +55,24 @@ static F parse(const std::string& h) {
   return r;
 }
 // "madd" / "maddn" mode: stdin lines "X Y ZZ ZZZ x2 y2" (hex) -> "X3 Y3 ZZ3 ZZZ3" of
-// state + (x2, y2) / state + (x2, -y2)
-static bool g_neg = false;
+// state + (x2, y2) / state + (x2, -y2).  "maddl" / "maddln": the round-6 loop's pair -- an
+// identity state takes start(x2, +-y2), any other madd_live; a cancellation prints all-zero limbs
+// (the loop then marks its chain empty, i.e. the identity).
+static bool g_neg = false, g_live = false;
 static int madd_mode() {
   char buf[6][80];
   while (scanf("%79s %79s %79s %79s %79s %79s", buf[0], buf[1], buf[2], buf[3], buf[4], buf[5]) == 6) {
     const Xyzz st{parse(buf[0]), parse(buf[1]), parse(buf[2]), parse(buf[3])};
-    const Xyzz r = madd(st, parse(buf[4]), parse(buf[5]), g_neg);
+    Xyzz r;
+    if (!g_live) {
+      r = madd(st, parse(buf[4]), parse(buf[5]), g_neg);
+    } else if (is_identity(st)) {
+      r = start(parse(buf[4]), parse(buf[5]), g_neg);
+    } else {
+      bool cancel = false;
+      r = madd_live(st, parse(buf[4]), parse(buf[5]), g_neg, cancel);
+      if (cancel) r = identity();
+    }
     pr(r.X), pr(r.Y), pr(r.ZZ), pr(r.ZZZ);
     printf("\n");
   }
@@ -100,6 +111,16 @@ static int run_ops(bool fq) {
     pr(a), pr(b), pr(sub<8>(a, b));
     printf("\nsub2c6");
     pr(a), pr(b), pr(c), pr(sub_2c<6>(a, b, c));
+    printf("\nmul_sub8");  // c below 8p (a csub chain bound it below 4p, then + up to 3p)
+    {
+      const F29<M> c8 = csub<4>(c);
+      pr(a), pr(b), pr(c8), pr(mul_sub<8>(a, b, c8));
+    }
+    printf("\nsqr_sub2c6");  // b below 2p, c below 2p (the chain's PPP and Q)
+    {
+      const F29<M> b2 = csub<1>(csub<2>(csub<4>(b))), c2 = csub<1>(csub<2>(csub<4>(d)));
+      pr(a), pr(b2), pr(c2), pr(sqr_sub2c<6>(a, b2, c2));
+    }
     printf("\ncsub1");
     pr(a), pr(csub<1>(a));
     printf("\ncsub2");
@@ -164,6 +185,8 @@ static int xadd_mode() {
 int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "madd")) return madd_mode();
   if (argc > 1 && !strcmp(argv[1], "maddn")) return g_neg = true, madd_mode();
+  if (argc > 1 && !strcmp(argv[1], "maddl")) return g_live = true, madd_mode();
+  if (argc > 1 && !strcmp(argv[1], "maddln")) return g_live = g_neg = true, madd_mode();
   if (argc > 1 && !strcmp(argv[1], "xadd")) return xadd_mode();
   const bool fr = argc > 1 && !strcmp(argv[1], "fr");  // the same checks over Fr (FrM29)
   return fr ? run_ops<FrM29>(false) : run_ops<FqM29>(true);

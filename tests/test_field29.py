@@ -63,6 +63,16 @@ def test_field_ops_values_and_bounds(f29, field):
                 want = ins[0] * ins[1] + ins[2] * ins[3]
             assert r < 2 * P, line
             assert r % P == want * RINV % P, line
+        elif op == "mul_sub8":
+            a, b, c, r = v
+            if a >= 12 * P or b >= 12 * P or c >= 8 * P:
+                continue
+            assert 0 <= r < 10 * P and r % P == (a * b * RINV - c) % P, line
+        elif op == "sqr_sub2c6":
+            a, b, c, r = v
+            if a >= 12 * P or b >= 2 * P or c >= 2 * P:
+                continue
+            assert 0 < r < 8 * P and r % P == (a * a * RINV - b - 2 * c) % P, line
         elif op == "sub2c6":
             a, b, c, r = v
             want = a + 6 * P - b - 2 * c
@@ -103,6 +113,7 @@ def test_field_ops_values_and_bounds(f29, field):
     assert counts.get("zero6", 0) >= (3006 if field == "fq" else 0)
     assert counts.get("zero10", 0) >= (3010 if field == "fq" else 0)
     assert counts.get("sub2c6", 0) >= 3000 and counts.get("sub8", 0) >= 3000
+    assert counts.get("mul_sub8", 0) >= 3000 and counts.get("sqr_sub2c6", 0) >= 3000
 
 
 def _state(pt, rng, identity=False, xmax=4):
@@ -125,8 +136,9 @@ def _to_affine(X, Y, ZZ, ZZZ):
     return (X * pow(ZZ, -1, P) % P, Y * pow(ZZZ, -1, P) % P)
 
 
+@pytest.mark.parametrize("live", [False, True])
 @pytest.mark.parametrize("neg", [False, True])
-def test_madd_group_law(f29, neg):
+def test_madd_group_law(f29, neg, live):
     """state + (x2, +-y2): the chain's signed point (neg folds the sign into S2 = y2 ZZZ)."""
     rng = random.Random(29 + neg)
     g = (1, 2)
@@ -146,7 +158,8 @@ def test_madd_group_law(f29, neg):
         yb = yv * RP % P + rng.randrange(2) * P
         cases.append((st, xb, yb, want))
     inp = "\n".join(" ".join(hex(v) for v in (*st, xb, yb)) for st, xb, yb, _ in cases) + "\n"
-    out = subprocess.run([f29, "maddn" if neg else "madd"], input=inp, capture_output=True, text=True,
+    mode = ("maddl" if live else "madd") + ("n" if neg else "")  # live: start / madd_live (round 6)
+    out = subprocess.run([f29, mode], input=inp, capture_output=True, text=True,
                          check=True).stdout.splitlines()
     assert len(out) == len(cases)
     for (st, xb, yb, want), line in zip(cases, out):

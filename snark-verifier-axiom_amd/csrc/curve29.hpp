@@ -68,7 +68,17 @@ SV29_HD Xyzz madd(const Xyzz& p, const F& x2, const F& y2) { return madd(p, x2, 
 // no identity-valued exit -- the merges those needed cost ~100 VALU instructions per entry (register
 // copies, 36 zeroing moves, the identity branch).  P + (-P) sets `cancel` and leaves a meaningless
 // state: the caller marks the chain empty and restarts it with its next point.
-SV29_HD Xyzz start(const F& x2, const F& y2, bool neg) { return {x2, neg ? sub<2>(zero(), y2) : y2, one(), one()}; }
+// (x2, -y2) starts as (x2, y2, 1, -1): y = Y / ZZZ, and ZZ^3 = ZZZ^2 still holds (Z = -1), so the sign
+// is a choice between two constants for ZZZ instead of a subtraction pass over y2
+SV29_HD F neg_one() {  // p - R' mod p
+  F r;
+  constexpr uint32_t O[L] = {0x3003126u, 0xce8395eu, 0x420727bu, 0x1891eb7u, 0xae269bfu,
+                             0x598fff2u, 0xed19539u, 0x9315e8bu, 0x229c18u};
+#pragma unroll
+  for (int i = 0; i < L; i++) r.v[i] = O[i];
+  return r;
+}
+SV29_HD Xyzz start(const F& x2, const F& y2, bool neg) { return {x2, y2, one(), neg ? neg_one() : one()}; }
 SV29_HD Xyzz madd_live(const Xyzz& p, const F& x2, const F& y2, bool neg, bool& cancel) {
   F Pd = mul_sub<8>(x2, p.ZZ, p.X);                  // U2 - X + 8p, fused: < 10p (state X < 8p)
   F Rd = sub_sgn<4>(mul(y2, p.ZZZ), neg, p.Y);       // +-S2 - Y + 4p: < 6p
@@ -76,7 +86,10 @@ SV29_HD Xyzz madd_live(const Xyzz& p, const F& x2, const F& y2, bool neg, bool& 
   bool dbl = false;
   if (is_zero_mod_p_10p(Pd)) {
     if (!is_zero_mod_p_6p(Rd)) {
-      cancel = true;  // P + (-P): the caller restarts the chain (the products below run on as garbage)
+      // P + (-P): the caller restarts the chain.  The products below run on as garbage except
+      // ZZ3 = 0 * PP = 0 exactly, so the state reads as the identity (ZZ == 0) if it is stored
+      cancel = true;
+      ZZ = zero();
     } else {
       const F x2s = sqr(x2), ys = neg ? sub<2>(zero(), y2) : y2;
       Pd = add(ys, ys);               // < 4p

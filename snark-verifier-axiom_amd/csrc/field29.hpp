@@ -414,30 +414,22 @@ SV29_HD bool is_zero(const F29<M>& a) {
   return x == 0;
 }
 
-// a == 0 mod p for a below 6p: a in {0, p, .., 5p} (Fq only: LOW holds p's multiples).  The low
-// limb filters (a match of limb 0 with one of the six multiples is needed), so the full comparisons
-// run only on that rare path.
-SV29_HD bool is_zero_mod_p_6p(const F& a) {
-  constexpr uint32_t LOW[6] = {0u, 0x187cfd47u, 0x10f9fa8eu, 0x976f7d5u, 0x1f3f51cu, 0x1a70f263u};
-  bool cand = false;
-#pragma unroll
-  for (int k = 0; k < 6; k++) cand |= a.v[0] == LOW[k];
-  if (!cand) return false;
-  // rare: reduce below p by conditional subtractions of 4p, 2p, p (a < 6p < 8p)
-  return is_zero(csub<1>(csub<2>(csub<4>(a))));
-}
-
-// a == 0 mod p for a below 10p (round 5: the bucket chain's Pd = U2 - X + 8p with X below 8p)
-SV29_HD bool is_zero_mod_p_10p(const F& a) {
-  constexpr uint32_t LOW[10] = {0u,         0x187cfd47u, 0x10f9fa8eu, 0x976f7d5u,  0x1f3f51cu,
-                                0x1a70f263u, 0x12edefaau, 0xb6aecf1u,  0x3e7ea38u,  0x1c64e77fu};
-  bool cand = false;
-#pragma unroll
-  for (int k = 0; k < 10; k++) cand |= a.v[0] == LOW[k];
-  if (!cand) return false;
-  // rare: reduce below p by conditional subtractions of 8p, 4p, 2p, p (a < 10p < 16p)
+// a == 0 mod p for a below 16p (Fq only): a in {0, p, .., 15p}.  Round 6: the one multiple k p a
+// can equal comes from its top limb, k = round(a_8 / (p / 2^232)) in float (the multiples' top
+// limbs are ~3.17e6 apart, so the rounding is exact for every k < 16; tests/test_field29.py checks
+// all sixteen), and limb 0 must match k p's; the full comparison runs only on that rare path.  The
+// round-5 filter compared limb 0 with each multiple, which the compiler lowered to a binary search
+// of divergent branches: ~60 SALU instructions per bucket entry.
+SV29_HD bool is_zero_mod_p_16p(const F& a) {
+  constexpr float kInvPTop = 3.1531752142655023e-07f;  // 2^232 / p
+  const uint32_t k = (uint32_t)((float)a.v[L - 1] * kInvPTop + 0.5f);
+  if (a.v[0] != ((k * FqM29::kp(1, 0)) & MASK)) return false;
+  // rare: reduce below p by conditional subtractions of 8p, 4p, 2p, p
   return is_zero(csub<1>(csub<2>(csub<4>(csub<8>(a)))));
 }
+SV29_HD bool is_zero_mod_p_6p(const F& a) { return is_zero_mod_p_16p(a); }
+// (round 5: the bucket chain's Pd = U2 - X + 8p with X below 8p is below 10p)
+SV29_HD bool is_zero_mod_p_10p(const F& a) { return is_zero_mod_p_16p(a); }
 
 // Form changes without a product: x R' = 32 (x R) mod p, so the way in is a 5-bit shift and a
 // small reduction, the way out an exact division by 32 (a Montgomery reduction by 2^5).

@@ -89,15 +89,6 @@ __device__ __forceinline__ G1Aff load_vpoint(const G1Aff* __restrict__ bases, co
   return r;
 }
 
-// all-zero words: the identity in both stored forms (ZZ = 0)
-__device__ __forceinline__ G1Xyzz zero_xyzz() {
-  G1Xyzz r;
-  uint32_t* d = reinterpret_cast<uint32_t*>(&r);
-#pragma unroll
-  for (int k = 0; k < 32; k++) d[k] = 0;
-  return r;
-}
-
 __device__ __forceinline__ G1Xyzz load_xyzz(const G1Xyzz* __restrict__ a, uint32_t i) {
   const uint4* p = reinterpret_cast<const uint4*>(a + i);
   G1Xyzz r;
@@ -330,38 +321,52 @@ __global__ void k_glv_phix(const G1Aff* __restrict__ bases, uint32_t n, uint4* _
   if (i < n) glv_phix(bases, i, phix, phi64, err);
 }
 
-// The 29-bit chain's table of virtual points (p.r29, replaces phix): every record in x R' words
-// (AccChain's storage form), so the accumulate's per-entry point conversion is a limb split --
-// converted once per point here instead of once per bucket entry (16 entries per point at 2^20).
-// P_i at record i and, with GLV, phi(P_i) = (beta x_i, y_i) at record nsplit + i.  With err set the
-// bases are checked to be reduced (Montgomery input is used as is).
+// The 29-bit chain's table of virtual points (p.r29, replaces phix): every record the chain's own
+// limbs, x R' as 9 x 29-bit limbs for x then y (72 B, 9 uint2), so the accumulate's per-entry point
+// load is the whole conversion -- converted once per point here instead of once per bucket entry
+// (16 entries per point at 2^20).  Round 6: the limbs themselves (round 4-5 stored 8-word x R'
+// values, 64 B, and split them into limbs per entry: ~35 VALU instructions per entry).  P_i at
+// record i and, with GLV, phi(P_i) = (beta x_i, y_i) at record nsplit + i.  With err set the bases
+// are checked to be reduced (Montgomery input is used as is).
 static constexpr int kPhiVtab = 2;  // k_bin_hist's phi64 value for "phix is the r29 table"
-__device__ __forceinline__ void st_words(uint4* o, const Fq& w) {
-  o[0] = make_uint4(w.v[0], w.v[1], w.v[2], w.v[3]);
-  o[1] = make_uint4(w.v[4], w.v[5], w.v[6], w.v[7]);
+static constexpr int kVtabRec = 9;  // uint2 per record
+__device__ __forceinline__ void st_rec29(uint2* o, const r29::F& x, const r29::F& y) {
+  o[0] = make_uint2(x.v[0], x.v[1]);
+  o[1] = make_uint2(x.v[2], x.v[3]);
+  o[2] = make_uint2(x.v[4], x.v[5]);
+  o[3] = make_uint2(x.v[6], x.v[7]);
+  o[4] = make_uint2(x.v[8], y.v[0]);
+  o[5] = make_uint2(y.v[1], y.v[2]);
+  o[6] = make_uint2(y.v[3], y.v[4]);
+  o[7] = make_uint2(y.v[5], y.v[6]);
+  o[8] = make_uint2(y.v[7], y.v[8]);
 }
+__device__ __forceinline__ void ld_rec29(const uint2* __restrict__ o, r29::F& x, r29::F& y) {
+  uint2 q[kVtabRec];
+#pragma unroll
+  for (int k = 0; k < kVtabRec; k++) q[k] = o[k];
+  x.v[0] = q[0].x, x.v[1] = q[0].y, x.v[2] = q[1].x, x.v[3] = q[1].y, x.v[4] = q[2].x, x.v[5] = q[2].y;
+  x.v[6] = q[3].x, x.v[7] = q[3].y, x.v[8] = q[4].x;
+  y.v[0] = q[4].y, y.v[1] = q[5].x, y.v[2] = q[5].y, y.v[3] = q[6].x, y.v[4] = q[6].y, y.v[5] = q[7].x;
+  y.v[6] = q[7].y, y.v[7] = q[8].x, y.v[8] = q[8].y;
+}
+// uint4 per point of the r29 table (its buffer is carved in uint4): GLV two 72-B records, else one
+// (padded to 80 B per point so host-fed pieces' table slices stay uint4-aligned)
+__host__ __device__ constexpr size_t vtab_uint4_per_point(bool glv) { return glv ? 9 : 5; }
 __device__ __forceinline__ void vtab_put(const G1Aff* __restrict__ bases, uint32_t i, uint4* __restrict__ vtab,
                                          uint32_t nsplit, bool glv, uint32_t* __restrict__ err) {
   const G1Aff a = load_aff(bases, i);
   if (err && (!a.x.is_reduced() || !a.y.is_reduced())) atomicOr(err, 1u);
-  const Fq y = fq_to_r29w(a.y);
-  const r29::F x = r29::to_r29(a.x.v);
-  Fq xw;
-  r29::to_words(x, xw.v);
-  uint4* o = vtab + 4 * (size_t)i;
-  st_words(o, xw);
-  st_words(o + 2, y);
+  const r29::F y = r29::to_r29(a.y.v), x = r29::to_r29(a.x.v);  // below 2p
+  uint2* t = reinterpret_cast<uint2*>(vtab);
+  st_rec29(t + kVtabRec * (size_t)i, x, y);
   if (glv) {  // beta x in the 29-bit form directly: beta R' (GLV_BETA_MONT re-expressed, 2^261)
     constexpr uint32_t kBeta29[r29::L] = {0xa337995u, 0x158d1d23u, 0x189c9b98u, 0x12fa4e45u, 0x185faadcu,
                                          0x176f16du, 0xeed93bau,  0x14291140u, 0xc0afeu};
     r29::F beta;
 #pragma unroll
     for (int j = 0; j < r29::L; j++) beta.v[j] = kBeta29[j];
-    Fq bw;
-    r29::to_words(r29::mul(x, beta), bw.v);  // below 2p
-    uint4* q = vtab + 4 * ((size_t)nsplit + i);
-    st_words(q, bw);
-    st_words(q + 2, y);
+    st_rec29(t + kVtabRec * ((size_t)nsplit + i), r29::mul(x, beta), y);  // below 2p
   }
 }
 // Host-fed pieces with the 29-bit chain: the piece's table once its bases have landed
@@ -913,11 +918,11 @@ struct AccChain<true> {
 #ifndef SV_ACC29_MIN_BLOCKS
 #define SV_ACC29_MIN_BLOCKS 4
 #endif
-// NL (round 6, the 29-bit chain only; SVGPU_ACC_LOOP=0 keeps the round-5 loop): the chain's state
+// NL (round 6, the 29-bit chain; the round-5 loop stays for the 32-bit chain only): the chain's state
 // is never the identity -- a lane whose chain is empty (segment start, or after P + (-P)) takes its
 // next point as the state in the loop's divergent segment-end block and skips that entry's madd, so
 // the per-entry step is r29::madd_live with no identity test or identity-valued merge.
-template <bool ADD, bool R29, int PF = SV_ACC_PREFETCH, bool NL = R29>
+template <bool ADD, bool R29, int PF = SV_ACC_PREFETCH, bool NL = R29>  // (R29 implies NL)
 __global__ void __launch_bounds__(kBlock, R29 ? SV_ACC29_MIN_BLOCKS : SV_ACC_MIN_BLOCKS) k_accumulate(
     const G1Aff* __restrict__ bases, const uint32_t* __restrict__ ent, const uint32_t* __restrict__ gst,
     const uint32_t* __restrict__ tstart, uint32_t nbt, uint32_t K, uint32_t T,
@@ -958,17 +963,21 @@ __global__ void __launch_bounds__(kBlock, R29 ? SV_ACC29_MIN_BLOCKS : SV_ACC_MIN
     if constexpr (PF >= 2) pnext = load_vpoint(bases, phix, vnext & 0x7fffffffu, nsplit, phi64);
     if constexpr (NL) {
       static_assert(R29 && PF == 1, "the restructured loop is the 29-bit chain's");
+      (void)bases;
+      (void)nsplit;
+      (void)phi64;
       for (uint32_t e = s0; e < e_end; e++) {
         // the entry's point first: a segment starting here starts from it
         const uint32_t v = vnext;
         if (e + 1 < e_end) vnext = ent[e + 1];
-        const G1Aff p = load_vpoint(bases, phix, v & 0x7fffffffu, nsplit, phi64);
-        const bool live = !p.is_identity(), neg = (v & 0x80000000u) != 0;
-        const r29::F x = r29::from_words(p.x.v), y = r29::from_words(p.y.v);  // the table's x R' words
+        r29::F x, y;  // the table's limbs (the identity: all-zero limbs)
+        ld_rec29(reinterpret_cast<const uint2*>(phix) + (size_t)kVtabRec * (v & 0x7fffffffu), x, y);
+        const bool live = !(r29::is_zero(x) && r29::is_zero(y)), neg = (v & 0x80000000u) != 0;
         bool fresh = false;
         if (e >= ge || empty) {  // divergent: a segment ends here, or the chain is empty
           if (e >= ge) {  // segment [seg_start, ge) of bucket g ends inside this chunk
-            const G1Xyzz sum = empty ? zero_xyzz() : A::out(acc);
+            // an empty chain has acc.ZZ == 0 (set below / by madd_live's cancellation): the identity
+            const G1Xyzz sum = A::out(acc);
             if (seg_start == gs) {
               store_xyzz(bsum, g, sum);
             } else {  // head piece of a bucket owned by an earlier thread
@@ -986,6 +995,8 @@ __global__ void __launch_bounds__(kBlock, R29 ? SV_ACC29_MIN_BLOCKS : SV_ACC_MIN
             if constexpr (ADD) {
               acc = A::in(load_xyzz(bsum, g));
               empty = r29::is_zero(acc.ZZ);
+            } else {
+              acc.ZZ = r29::zero();
             }
           }
           if (empty && live) {
@@ -1040,8 +1051,7 @@ __global__ void __launch_bounds__(kBlock, R29 ? SV_ACC29_MIN_BLOCKS : SV_ACC_MIN
       }
       if (!p.is_identity()) acc = A::madd(acc, p, (v & 0x80000000u) != 0);
     }
-    if constexpr (NL) sum = empty ? zero_xyzz() : A::out(acc);
-    else sum = A::out(acc);
+    sum = A::out(acc);  // (NL: an empty chain has acc.ZZ == 0, the identity)
     if (seg_start == gs && e_end == ge) {
       store_xyzz(bsum, g, sum);
     } else if (seg_start != gs) {  // first segment, bucket started earlier (it may also go on later)
@@ -1827,16 +1837,9 @@ static int msm_acc(const MsmPlan& p, const MsmScratch& w, const SortOut& so, con
   // (a point prefetch one entry ahead, k_accumulate<., ., 2>, measured no gain on the device path or
   // on the host-fed pieces' ~2 waves per SIMD: 2^20 host-fed 2.69-2.71 ms either way)
   const int r29 = p.r29;
-  if (r29) {  // phix is the 29-bit chain's table of every virtual point (vtab_put): read record idx
-    bases = reinterpret_cast<const G1Aff*>(phix);
-    phix = nullptr;
-    nsplit = ~0u;
-  }
-  const bool old_loop = getenv("SVGPU_ACC_LOOP") && atoi(getenv("SVGPU_ACC_LOOP")) == 0;  // read per call
-  auto kern = add_into ? (r29 ? (old_loop ? k_accumulate<true, true, SV_ACC_PREFETCH, false> : k_accumulate<true, true>)
-                              : k_accumulate<true, false>)
-                       : (r29 ? (old_loop ? k_accumulate<false, true, SV_ACC_PREFETCH, false> : k_accumulate<false, true>)
-                              : k_accumulate<false, false>);
+  if (r29) nsplit = ~0u;  // phix is the 29-bit chain's table of every virtual point (vtab_put): record idx
+  auto kern = add_into ? (r29 ? k_accumulate<true, true> : k_accumulate<true, false>)
+                       : (r29 ? k_accumulate<false, true> : k_accumulate<false, false>);
   hipLaunchKernelGGL(kern, dim3(cdiv(so.T, kBlock)), dim3(kBlock), 0, st, bases, so.ent, so.gst, so.tstart, nbt,
                      so.K, so.T, bsum, w.pfirst, w.plast, w.multi, w.nmulti, w.heavy, w.nheavy, phix, nsplit,
                      p.phi64);
@@ -1988,7 +1991,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   const bool conv = (form == SV_CANONICAL);
   if (conv) add(n * sizeof(G1Aff));
   // GLV: beta x (or phi(P)) per point; the 29-bit chain: its table of every virtual point instead
-  const size_t tab4 = p.r29 ? (p.glv ? 8 : 4) : (p.glv ? (p.phi64 ? 4 : 2) : 0);  // uint4 per point
+  const size_t tab4 = p.r29 ? vtab_uint4_per_point(p.glv) : (p.glv ? (p.phi64 ? 4 : 2) : 0);  // uint4 per point
   if (tab4) add(n * tab4 * sizeof(uint4));
   const size_t nfinal = (size_t)p.W * p.NG;
   uint32_t gparts = nfinal < 256 ? 2 : 1;      // k_group_sum blocks per group (see there)

@@ -56,8 +56,8 @@ static F parse(const std::string& h) {
 }
 // "madd" / "maddn" mode: stdin lines "X Y ZZ ZZZ x2 y2" (hex) -> "X3 Y3 ZZ3 ZZZ3" of
 // state + (x2, y2) / state + (x2, -y2).  "maddl" / "maddln": the round-6 loop's pair -- an
-// identity state takes start(x2, +-y2), any other madd_live; a cancellation prints all-zero limbs
-// (the loop then marks its chain empty, i.e. the identity).
+// identity state takes start(x2, +-y2), any other madd_live; a cancelled state must have ZZ == 0 (the
+// loop marks its chain empty and a stored one reads as the identity), X and Y are left as they are.
 static bool g_neg = false, g_live = false;
 static int madd_mode() {
   char buf[6][80];
@@ -71,7 +71,7 @@ static int madd_mode() {
     } else {
       bool cancel = false;
       r = madd_live(st, parse(buf[4]), parse(buf[5]), g_neg, cancel);
-      if (cancel) r = identity();
+      if (cancel && !is_identity(r)) r.ZZ.v[0] = 1;  // the loop reads a cancelled state by ZZ == 0
     }
     pr(r.X), pr(r.Y), pr(r.ZZ), pr(r.ZZZ);
     printf("\n");
@@ -134,6 +134,9 @@ static int run_ops(bool fq) {
       printf("\nzero10 ");
       pr(a);
       printf(" %d", is_zero_mod_p_10p(a) ? 1 : 0);
+      printf("\nzero16 ");
+      pr(a);
+      printf(" %d", is_zero_mod_p_16p(a) ? 1 : 0);
     }
     uint32_t w[8], w2[8];
     to_words(a, w);
@@ -154,7 +157,7 @@ static int run_ops(bool fq) {
     printf("\n");
   }
   // zero tests on exact multiples of p
-  for (int k = 0; fq && k < 10; k++) {
+  for (int k = 0; fq && k < 16; k++) {
     F m = zero();
     for (int j = 0; j < k; j++) m = sub<1>(m, zero());  // m + p
     if (k < 6) {
@@ -162,9 +165,23 @@ static int run_ops(bool fq) {
       pr(m);
       printf(" %d\n", is_zero_mod_p_6p(m) ? 1 : 0);
     }
-    printf("zero10 ");
+    if (k < 10) {
+      printf("zero10 ");
+      pr(m);
+      printf(" %d\n", is_zero_mod_p_10p(m) ? 1 : 0);
+    }
+    printf("zero16 ");
     pr(m);
-    printf(" %d\n", is_zero_mod_p_10p(m) ? 1 : 0);
+    printf(" %d\n", is_zero_mod_p_16p(m) ? 1 : 0);
+    // neighbours of k p: limb 0 matches a multiple's, the value does not
+    for (int d : {-1, 1}) {
+      F n = m;
+      n.v[L - 1] += (uint32_t)d;  // k p +- 2^232: the top limb moves, limb 0 stays
+      if (k == 0 && d < 0) continue;
+      printf("zero16 ");
+      pr(n);
+      printf(" %d\n", is_zero_mod_p_16p(n) ? 1 : 0);
+    }
   }
   return 0;
 }

@@ -41,6 +41,7 @@
 #include <functional>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "curve.hpp"
@@ -108,44 +109,69 @@ __device__ __forceinline__ void store_xyzz(G1Xyzz* __restrict__ a, uint32_t i, c
   for (int k = 0; k < 8; k++) p[k] = make_uint4(s[4 * k], s[4 * k + 1], s[4 * k + 2], s[4 * k + 3]);
 }
 
-// r29w storage form (see AccChain) <-> canonical x R: one coordinate, one point
-// x R' words (below 4p) -> x R canonical: x R = (x R') / 32 mod p, an exact division of w + m p,
-// m = -w p^-1 mod 32 (p = 7 mod 32, -p^-1 = 9): eight v_mad_u64_u32 and eight funnel shifts
-__device__ __forceinline__ Fq fq_from_r29w(const Fq& w) {
-  const uint32_t m = (w.v[0] * 9u) & 31u;
-  uint32_t t[9];
-  uint64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    c = (uint64_t)m * FQ_P[i] + ((uint64_t)w.v[i] + (c >> 32));
-    t[i] = (uint32_t)c;
-  }
-  t[8] = (uint32_t)(c >> 32);
-  Fq r;
-#pragma unroll
-  for (int i = 0; i < 8; i++) r.v[i] = __builtin_amdgcn_alignbit(t[i + 1], t[i], 5);
-  return fe_canon2p(r);  // (w + m p) / 32 < (4p + 31p) / 32 < 2p
+// Bucket-sum records (bsum, pfirst, plast).  The 32-bit chain stores canonical G1Xyzz (128 B).  The
+// 29-bit chain (round 6) stores its own state as it is: 4 x 9 limbs, 144 B, X below 8p -- a segment
+// end is nine 16-B stores and no conversion (round 4-5 packed the limbs into 8-word x R' values
+// after a conditional subtraction of 4p: ~110 VALU instructions in the accumulate's divergent
+// segment-end block, i.e. ~70 per bucket entry at 2^20).  The readers convert once per bucket.
+// Arrays stay typed G1Xyzz*: rec_at gives record i of either form.
+constexpr uint32_t kRec29Words = 4 * r29::L;  // 36
+__host__ __device__ __forceinline__ size_t bucket_rec_bytes(int r29) { return r29 ? 4 * kRec29Words : sizeof(G1Xyzz); }
+template <class T>
+__host__ __device__ __forceinline__ T* rec_at(T* base, size_t i, int r29) {
+  using U = typename std::conditional<std::is_const<T>::value, const uint32_t, uint32_t>::type;
+  return r29 ? reinterpret_cast<T*>(reinterpret_cast<U*>(base) + kRec29Words * i) : base + i;
 }
-__device__ __forceinline__ Fq fq_to_r29w(const Fq& c) {  // x R canonical -> x R' words (below 2p)
+__device__ __forceinline__ void st_rec29(G1Xyzz* __restrict__ base, size_t i, const r29::Xyzz& a) {
+  uint4* o = reinterpret_cast<uint4*>(rec_at(base, i, 1));
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&a);
+#pragma unroll
+  for (int k = 0; k < 9; k++) o[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+}
+__device__ __forceinline__ r29::Xyzz ld_rec29(const G1Xyzz* __restrict__ base, size_t i) {
+  const uint4* o = reinterpret_cast<const uint4*>(rec_at(base, i, 1));
+  r29::Xyzz a;
+  uint32_t* w = reinterpret_cast<uint32_t*>(&a);
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    const uint4 q = o[k];
+    w[4 * k] = q.x, w[4 * k + 1] = q.y, w[4 * k + 2] = q.z, w[4 * k + 3] = q.w;
+  }
+  return a;
+}
+// one coordinate (0..3: X, Y, ZZ, ZZZ) of a 29-bit record in field.hpp's canonical x R form
+__device__ __forceinline__ Fq rec29_coord_canonical(const G1Xyzz* __restrict__ rec, int c) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(rec) + r29::L * c;
+  r29::F f;
+#pragma unroll
+  for (int i = 0; i < r29::L; i++) f.v[i] = w[i];
   Fq r;
-  r29::to_words(r29::to_r29(c.v), r.v);
+  r29::to_r32(r29::csub<4>(f), r.v);  // X below 8p; the others below 2p (csub leaves them)
   return r;
 }
-__device__ __forceinline__ G1Xyzz xyzz_from_r29w(const G1Xyzz& a) {
-  return {fq_from_r29w(a.X), fq_from_r29w(a.Y), fq_from_r29w(a.ZZ), fq_from_r29w(a.ZZZ)};
-}
-__device__ __forceinline__ G1Xyzz xyzz_to_r29w(const G1Xyzz& a) {
-  return {fq_to_r29w(a.X), fq_to_r29w(a.Y), fq_to_r29w(a.ZZ), fq_to_r29w(a.ZZZ)};
+__device__ __forceinline__ void rec29_coord_store(G1Xyzz* __restrict__ rec, int c, const Fq& canon) {
+  const r29::F f = r29::to_r29(canon.v);  // below 2p
+  uint32_t* w = reinterpret_cast<uint32_t*>(rec) + r29::L * c;
+#pragma unroll
+  for (int i = 0; i < r29::L; i++) w[i] = f.v[i];
 }
 __device__ __forceinline__ G1Xyzz load_bucket(const G1Xyzz* __restrict__ a, uint32_t i, int r29w) {
-  G1Xyzz v = load_xyzz(a, i);
-  if (r29w) {
-    v.X = fq_from_r29w(v.X);
-    v.Y = fq_from_r29w(v.Y);
-    v.ZZ = fq_from_r29w(v.ZZ);
-    v.ZZZ = fq_from_r29w(v.ZZZ);
+  if (!r29w) return load_xyzz(a, i);
+  const G1Xyzz* rec = rec_at(a, i, 1);
+  return {rec29_coord_canonical(rec, 0), rec29_coord_canonical(rec, 1), rec29_coord_canonical(rec, 2),
+          rec29_coord_canonical(rec, 3)};
+}
+// store a canonical sum into record i of either form
+__device__ __forceinline__ void store_bucket(G1Xyzz* __restrict__ a, uint32_t i, const G1Xyzz& v, int r29w) {
+  if (!r29w) {
+    store_xyzz(a, i, v);
+    return;
   }
-  return v;
+  G1Xyzz* rec = rec_at(a, i, 1);
+  rec29_coord_store(rec, 0, v.X);
+  rec29_coord_store(rec, 1, v.Y);
+  rec29_coord_store(rec, 2, v.ZZ);
+  rec29_coord_store(rec, 3, v.ZZZ);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -930,7 +956,9 @@ __global__ void __launch_bounds__(kBlock, R29 ? SV_ACC29_MIN_BLOCKS : SV_ACC_MIN
     uint32_t* __restrict__ multi, uint32_t* __restrict__ nmulti, uint32_t* __restrict__ heavy,
     uint32_t* __restrict__ nheavy, const uint4* __restrict__ phix, uint32_t nsplit, int phi64) {
   using A = AccChain<R29>;
-  __shared__ G1Xyzz shead[kBlock];
+  // head pieces for the in-block join: canonical G1Xyzz (32-bit chain) or 29-bit records (144 B)
+  __shared__ G1Xyzz shead[R29 ? 1 : kBlock];
+  __shared__ uint4 shead29[R29 ? 9 * kBlock : 1];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t m = gst[nbt];
   const uint32_t s0 = t * K;
@@ -953,8 +981,12 @@ __global__ void __launch_bounds__(kBlock, R29 ? SV_ACC29_MIN_BLOCKS : SV_ACC_MIN
     bool empty = true;  // NL: the chain holds no point yet (acc is not read)
     if constexpr (ADD) {
       if (s0 == gs) {
-        acc = A::in(load_xyzz(bsum, g));
-        if constexpr (NL) empty = r29::is_zero(acc.ZZ);
+        if constexpr (R29) {
+          acc = ld_rec29(bsum, g);
+          empty = r29::is_zero(acc.ZZ);
+        } else {
+          acc = A::in(load_xyzz(bsum, g));
+        }
       }
     }
     uint32_t vnext = 0;
@@ -976,13 +1008,13 @@ __global__ void __launch_bounds__(kBlock, R29 ? SV_ACC29_MIN_BLOCKS : SV_ACC_MIN
         bool fresh = false;
         if (e >= ge || empty) {  // divergent: a segment ends here, or the chain is empty
           if (e >= ge) {  // segment [seg_start, ge) of bucket g ends inside this chunk
-            // an empty chain has acc.ZZ == 0 (set below / by madd_live's cancellation): the identity
-            const G1Xyzz sum = A::out(acc);
+            // the state as it is (an empty chain has acc.ZZ == 0, set below / by madd_live's
+            // cancellation: the identity)
             if (seg_start == gs) {
-              store_xyzz(bsum, g, sum);
+              st_rec29(bsum, g, acc);
             } else {  // head piece of a bucket owned by an earlier thread
-              if (join_in_block(gs, ge, K)) shead[threadIdx.x] = sum;
-              else store_xyzz(pfirst, t, sum);
+              if (join_in_block(gs, ge, K)) st_rec29(reinterpret_cast<G1Xyzz*>(shead29), threadIdx.x, acc);
+              else st_rec29(pfirst, t, acc);
             }
             first = false;
             do {
@@ -993,7 +1025,7 @@ __global__ void __launch_bounds__(kBlock, R29 ? SV_ACC29_MIN_BLOCKS : SV_ACC_MIN
             seg_start = e;
             empty = true;
             if constexpr (ADD) {
-              acc = A::in(load_xyzz(bsum, g));
+              acc = ld_rec29(bsum, g);
               empty = r29::is_zero(acc.ZZ);
             } else {
               acc.ZZ = r29::zero();
@@ -1051,24 +1083,31 @@ __global__ void __launch_bounds__(kBlock, R29 ? SV_ACC29_MIN_BLOCKS : SV_ACC_MIN
       }
       if (!p.is_identity()) acc = A::madd(acc, p, (v & 0x80000000u) != 0);
     }
-    sum = A::out(acc);  // (NL: an empty chain has acc.ZZ == 0, the identity)
+    if constexpr (!R29) sum = A::out(acc);
     if (seg_start == gs && e_end == ge) {
-      store_xyzz(bsum, g, sum);
+      if constexpr (R29) st_rec29(bsum, g, acc);
+      else store_xyzz(bsum, g, sum);
     } else if (seg_start != gs) {  // first segment, bucket started earlier (it may also go on later)
-      if (join_in_block(gs, ge, K)) shead[threadIdx.x] = sum;
-      else store_xyzz(pfirst, t, sum);
+      if constexpr (R29) {
+        if (join_in_block(gs, ge, K)) st_rec29(reinterpret_cast<G1Xyzz*>(shead29), threadIdx.x, acc);
+        else st_rec29(pfirst, t, acc);
+      } else {
+        if (join_in_block(gs, ge, K)) shead[threadIdx.x] = sum;
+        else store_xyzz(pfirst, t, sum);
+      }
     } else if (join_in_block(gs, ge, K)) {  // this thread owns a two-piece in-block bucket
       owner = true;
     } else {
-      store_xyzz(first ? pfirst : plast, t, sum);
+      if constexpr (R29) st_rec29(first ? pfirst : plast, t, acc);
+      else store_xyzz(first ? pfirst : plast, t, sum);
       multi[atomicAdd(nmulti, 1u)] = g;  // joined by k_fixup
       if ((ge - 1) / K - gs / K > kFixSerial) heavy[atomicAdd(nheavy, 1u)] = g;
     }
   }
   __syncthreads();
   if (owner) {
-    if constexpr (R29)
-      store_xyzz(bsum, g, xyzz_to_r29w(xyzz_add(xyzz_from_r29w(sum), xyzz_from_r29w(shead[threadIdx.x + 1]))));
+    if constexpr (R29)  // the two pieces added in the chain's own form (r29::add takes X below 12p)
+      st_rec29(bsum, g, r29::add(acc, ld_rec29(reinterpret_cast<const G1Xyzz*>(shead29), threadIdx.x + 1)));
     else
       store_xyzz(bsum, g, xyzz_add(sum, shead[threadIdx.x + 1]));
   }
@@ -1108,16 +1147,16 @@ __global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ g
       const uint32_t s = gst[g], e = gst[g + 1];
       const uint32_t t0 = s / K, t1 = (e - 1) / K;
       if (t1 - t0 > kFixSerial) continue;  // a heavy bucket: the other blocks' part
-      // r29w (k_accumulate's 29-bit chain): pieces and the stored sum in x R' words
-      Fq acc = quad::ld(s == t0 * K ? pfirst + t0 : plast + t0, c);
-      if (r29w) acc = fq_from_r29w(acc);
+      // r29w (k_accumulate's 29-bit chain): pieces and the stored sum as 29-bit records
+      const G1Xyzz* h0 = s == t0 * K ? pfirst : plast;
+      Fq acc = r29w ? rec29_coord_canonical(rec_at(h0, t0, 1), c) : quad::ld(h0 + t0, c);
       for (uint32_t t = t0 + 1; t <= t1; t++) {
-        Fq v = quad::ld(pfirst + t, c);
-        if (r29w) v = fq_from_r29w(v);
+        const Fq v = r29w ? rec29_coord_canonical(rec_at(pfirst, t, 1), c) : quad::ld(pfirst + t, c);
         acc = quad::add_2p(acc, v, c);
       }
       acc = fe_canon2p(acc);
-      quad::st(bsum + g, c, r29w ? fq_to_r29w(acc) : acc);
+      if (r29w) rec29_coord_store(rec_at(bsum, g, 1), c, acc);
+      else quad::st(bsum + g, c, acc);
     }
     return;
   }
@@ -1136,7 +1175,7 @@ __global__ void __launch_bounds__(kBlock) k_fixup(const uint32_t* __restrict__ g
     }
     if (tid == 0) {
       const G1Xyzz sum = xyzz_add(fixup_head(pfirst, plast, s, t0, K, r29w), sh[0]);
-      store_xyzz(bsum, g, r29w ? xyzz_to_r29w(sum) : sum);
+      store_bucket(bsum, g, xyzz_canon2p(sum), r29w);
     }
     __syncthreads();
   }
@@ -1153,11 +1192,11 @@ __device__ __forceinline__ bool bucket_at(const G1Xyzz* __restrict__ x, const ui
   return true;
 }
 
-// bucket i in the 29-bit chain's own form (r29w words -> limbs, no conversion); false when empty
+// bucket i in the 29-bit chain's own form (its record as stored: no conversion); false when empty
 __device__ __forceinline__ bool bucket_at29(const G1Xyzz* __restrict__ x, const uint32_t* __restrict__ gs, uint32_t i,
                                             r29::Xyzz& out) {
   if (gs && gs[i] == gs[i + 1]) return false;
-  out = AccChain<true>::in(load_xyzz(x, i));
+  out = ld_rec29(x, i);
   return true;
 }
 
@@ -1171,7 +1210,7 @@ __global__ void __launch_bounds__(kBlock) k_wsum(const G1Xyzz* __restrict__ X, c
   uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= J * groups) return;
   uint32_t g = tid / J, j = tid % J;
-  const G1Xyzz* x = X + (size_t)g * N;
+  const G1Xyzz* x = rec_at(X, (size_t)g * N, r29w);
   const uint32_t* gs = gst ? gst + (size_t)g * N : nullptr;
   uint32_t lo = j * L;
   uint32_t hi = min(N, lo + L);
@@ -1420,7 +1459,7 @@ __global__ void __launch_bounds__(kTreeN) k_wsum_tree(const G1Xyzz* __restrict__
   constexpr int kWhole = RUN ? 1 : 3;      // levels below this run as whole additions
   const uint32_t tid = threadIdx.x, bpw = J >> kTreeLog;
   const uint32_t g = blockIdx.x / bpw, j = (blockIdx.x % bpw) * kTreeN + tid;
-  const G1Xyzz* x = X + (size_t)g * N;
+  const G1Xyzz* x = rec_at(X, (size_t)g * N, r29w);
   const uint32_t* gs = gst ? gst + (size_t)g * N : nullptr;
   const bool odd = tid & 1;
   if constexpr (RUN) {
@@ -2011,8 +2050,9 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   add((((size_t)p.nbt + 1) * pieces + 1) * 4);  // gst per piece (+ 1: two window halves)
   add(entries * 4);                           // ent (every piece's sorted entries)
   add(tst_total * 4);                         // tstart per piece
-  add((size_t)Tmax * sizeof(G1Xyzz) * 2);     // pfirst, plast
-  add((size_t)p.nbt * sizeof(G1Xyzz));        // bsum
+  const size_t rec_bytes = bucket_rec_bytes(p.r29);  // bucket-sum records (29-bit chain: 144 B)
+  add((size_t)Tmax * rec_bytes * 2);          // pfirst, plast
+  add((size_t)p.nbt * rec_bytes);             // bsum
   add((size_t)p.nbt * 4);                     // heavy-bucket queue
   add((size_t)p.nbt * 4);                     // multi-thread-bucket queue
   add((size_t)p.J * p.W * sizeof(G1Xyzz) * 2);  // acc_j, T_j
@@ -2048,9 +2088,9 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
   uint32_t* gst_all = ws->carve<uint32_t>(((size_t)p.nbt + 1) * pieces + 1);
   uint32_t* ent_all = ws->carve<uint32_t>(entries);
   uint32_t* tst_all = ws->carve<uint32_t>(tst_total);
-  w.pfirst = ws->carve<G1Xyzz>(Tmax);
-  w.plast = ws->carve<G1Xyzz>(Tmax);
-  G1Xyzz* bsum = ws->carve<G1Xyzz>(p.nbt);
+  w.pfirst = reinterpret_cast<G1Xyzz*>(ws->carve<uint4>(Tmax * rec_bytes / 16));
+  w.plast = reinterpret_cast<G1Xyzz*>(ws->carve<uint4>(Tmax * rec_bytes / 16));
+  G1Xyzz* bsum = reinterpret_cast<G1Xyzz*>(ws->carve<uint4>(p.nbt * rec_bytes / 16));
   w.heavy = ws->carve<uint32_t>(p.nbt);
   w.multi = ws->carve<uint32_t>(p.nbt);
   w.nheavy = w.err + 1;  // zeroed with the error flag
@@ -2115,8 +2155,8 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
         sh[h].ent = ent_all + (h ? (size_t)p.npts * nwh[0] : 0);  // at most npts entries per window
         sh[h].gst = gst_all + (h ? (size_t)nwh[0] * p.B + 1 : 0);
         sh[h].tstart = tst_all + (h ? Th[0] + 1 : 0);
-        wh[h].pfirst = w.pfirst + (h ? Th[0] : 0);
-        wh[h].plast = w.plast + (h ? Th[0] : 0);
+        wh[h].pfirst = rec_at(w.pfirst, h ? Th[0] : 0, p.r29);
+        wh[h].plast = rec_at(w.plast, h ? Th[0] : 0, p.r29);
         wh[h].heavy = w.heavy + (h ? nwh[0] * p.B : 0);
         wh[h].multi = w.multi + (h ? nwh[0] * p.B : 0);
         wh[h].nheavy = w.err + 1 + 2 * h;
@@ -2133,7 +2173,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
       SV_TRY(msm_sort(p, w, sh[1], bases, scalars, n, mont_in, device, ss, nullptr, nsplit, 0, nullptr, nullptr,
                       nullptr, nullptr, nwh[0], nwh[1]));
       SV_HIP(hipEventRecord(ev[62], ss));
-      SV_TRY(msm_acc(p, wh[1], sh[1], bases, 0, ss, bsum + (size_t)nwh[0] * p.B, phix, nsplit, ev[63], nullptr,
+      SV_TRY(msm_acc(p, wh[1], sh[1], bases, 0, ss, rec_at(bsum, (size_t)nwh[0] * p.B, p.r29), phix, nsplit, ev[63], nullptr,
                      nwh[1] * p.B));
       SV_HIP(hipEventRecord(ev[8], ss));
       half_gst[0] = sh[0].gst;
@@ -2153,7 +2193,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
     // add into it).
     hipStream_t cs = ws->copy_stream, ss = ws->sort_stream;
     const bool prep_on_sort = !getenv("SVGPU_FED_PREP") || atoi(getenv("SVGPU_FED_PREP")) != 0;
-    if (pieces > 1) SV_HIP(hipMemsetAsync(bsum, 0, (size_t)p.nbt * sizeof(G1Xyzz), st));
+    if (pieces > 1) SV_HIP(hipMemsetAsync(bsum, 0, (size_t)p.nbt * rec_bytes, st));
     SV_HIP(hipEventRecord(ev[6], st));
     SV_HIP(hipStreamWaitEvent(cs, ev[6], 0));
     SV_HIP(hipStreamWaitEvent(ss, ev[6], 0));
@@ -2305,7 +2345,7 @@ static int msm_run_impl(const void* d_bases, const void* d_scalars, size_t n, in
     if (split) {
       reduce_windows(bsum, half_gst[0], 0, nwh[0]);  // beside half B's accumulate
       SV_HIP(hipStreamWaitEvent(st, ev[8], 0));
-      reduce_windows(bsum + (size_t)nwh[0] * p.B, half_gst[1], nwh[0], nwh[1]);
+      reduce_windows(rec_at(bsum, (size_t)nwh[0] * p.B, p.r29), half_gst[1], nwh[0], nwh[1]);
     } else {
       reduce_windows(bsum, pieces > 1 ? nullptr : so[0].gst, 0, p.W);
     }

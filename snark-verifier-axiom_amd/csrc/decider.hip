@@ -967,16 +967,21 @@ __device__ __forceinline__ void store_coeff(Fq2* __restrict__ dst, int k, int j,
   if (j < 2) st_fq(j ? &dst[k].c1 : &dst[k].c0, lz_reduce(v));
 }
 
-// dst = a * b (dst distinct from a and b)
-SV_WG_FN void w_mul(const WLane& L, Fq2* __restrict__ dst, const Fq2* a, const Fq2* b) {
+// OP_MUL's imm: multiply by the conjugate (odd w-coefficients negated) of operand a / b
+constexpr int kConjA = 1, kConjB = 2;
+// dst = a * b (dst distinct from a and b); conj (kConjA / kConjB): multiply by conj(a) / conj(b),
+// i.e. negate the terms of a's / b's odd w-coefficients -- a sign on the lane's multipliers
+SV_WG_FN void w_mul(const WLane& L, Fq2* __restrict__ dst, const Fq2* a, const Fq2* b, int conj = 0) {
   const int t = threadIdx.x;
   if (t < 192) {  // waves 0-2 (uniform per wave)
     const int q = L.mq;
     // q: 0 a0 b0 (re +), 1 a1 b1 (re -), 2 a0 b1 (im +), 3 a1 b0 (im +); idle lanes multiply by 0
     const Fq ax = ld_fq((q & 1) ? &a[L.mi].c1 : &a[L.mi].c0);
     const Fq by = ld_fq((q == 1 || q == 2) ? &b[L.mjj].c1 : &b[L.mjj].c0);
+    const bool flip = ((conj & kConjA) && (L.mi & 1)) != ((conj & kConjB) && (L.mjj & 1));
+    const uint32_t keep = flip ? 0u - L.mkeep : L.mkeep, send = flip ? 0u - L.msend : L.msend;
     // [0, 2p): the lane sums reduce once per coefficient
-    store_coeff(dst, L.mk, t & 31, lane_sum24<5>(fe_mul_lazy(ax, by), L.mkeep, L.msend));
+    store_coeff(dst, L.mk, t & 31, lane_sum24<5>(fe_mul_lazy(ax, by), keep, send));
   }
   __syncthreads();
 }
@@ -1094,19 +1099,17 @@ struct WProg {
   constexpr void op(WCode c, int d, int a, int b = 0, int imm = 0) {
     ops[n++] = WOp{(uint8_t)c, (uint8_t)imm, (uint16_t)d, (uint16_t)a, (uint16_t)b};
   }
-  // dst = a^x, x = BN_X in width-4 NAF; table of odd powers a, a^3, a^5, a^7 and their conjugates
-  // (= inverses on the cyclotomic subgroup); the chain ping-pongs between S_X0 and S_X1
+  // dst = a^x, x = BN_X in width-4 NAF; table of odd powers a, a^3, a^5, a^7 (a itself is entry 0,
+  // read where it lies); a negative digit multiplies by the entry's conjugate (the inverse on the
+  // cyclotomic subgroup), which OP_MUL applies as a sign of its odd-index terms (kConjB) -- round 6:
+  // no OP_COPY / OP_CONJ ops (15 per pow_x, ~800 cycles each); the chain ping-pongs between S_X0
+  // and S_X1
   constexpr void pow_x(int dst, int a) {
     const XNaf xn = make_xnaf();
     op(OP_SQR, S_X0, a);
-    op(OP_COPY, S_TAB, a);
-    op(OP_CONJ, S_TAB + 4, a);
-    for (int e = 1; e < 4; e++) {
-      op(OP_MUL, S_TAB + e, S_TAB + e - 1, S_X0);
-      op(OP_CONJ, S_TAB + 4 + e, S_TAB + e);
-    }
-    auto tab = [](int d) { return S_TAB + (d > 0 ? (d - 1) / 2 : 4 + (-d - 1) / 2); };
-    int r = tab(xn.d[xn.len - 1]);
+    for (int e = 1; e < 4; e++) op(OP_MUL, S_TAB + e, e == 1 ? a : S_TAB + e - 1, S_X0);
+    auto entry = [a](int d) { const int e = ((d > 0 ? d : -d) - 1) / 2; return e == 0 ? a : S_TAB + e; };
+    int r = entry(xn.d[xn.len - 1]);  // (the NAF's top digit is positive)
     for (int i = xn.len - 2; i >= 0; i--) {
       const int d = xn.d[i];
       const bool last_sq = i == 0 && d == 0;
@@ -1115,7 +1118,7 @@ struct WProg {
       r = s1;
       if (d) {
         const int s2 = i == 0 ? dst : (r == S_X0 ? S_X1 : S_X0);
-        op(OP_MUL, s2, r, tab(d));
+        op(OP_MUL, s2, r, entry(d), d < 0 ? kConjB : 0);
         r = s2;
       }
     }
@@ -1124,19 +1127,21 @@ struct WProg {
 constexpr WProg make_wprog(bool paired = false) {
   WProg P{};
   const StepTab st = make_steps();
-  P.op(OP_COPY, S_F0, st.x[0]);
+  int f = st.x[0];  // f starts as the first step's multiplier, read where it lies (no copy)
   int j = 1;
   if (paired) {  // f <- f^4 Y_p (see StepTab)
     for (int p = 0; p < kStepPairs; p++, j += 2) {
-      P.op(OP_SQR, S_T1, S_F0);
+      P.op(OP_SQR, S_T1, f);
       P.op(OP_SQR, S_F1, S_T1);
       P.op(OP_MUL, S_F0, S_F1, kOpY | p);
+      f = S_F0;
     }
   }
   // Miller loop, merged step multipliers as in k_decide_lanes: f <- f^2 * (D_idx or M_m)
   for (; j < st.n; j++) {
-    P.op(OP_SQR, S_F1, S_F0);
+    P.op(OP_SQR, S_F1, f);
     P.op(OP_MUL, S_F0, S_F1, st.x[j]);
+    f = S_F0;
   }
   P.op(OP_MUL, S_F1, S_F0, kOpM | st.m_final);  // the two Frobenius steps
   // Final exponentiation with NO inversion.  The easy part f^(p^6 - 1) = conj(f) / f is kept as the
@@ -1173,15 +1178,13 @@ constexpr WProg make_wprog(bool paired = false) {
   P.op(OP_MUL, S_L2, S_F0, S_A6);        // l2 = f a6
   P.op(OP_MUL, S_T0, S_Y36, S_A18);
   P.op(OP_MUL, S_T1, S_T0, S_B12);
-  P.op(OP_CONJ, S_T2, S_T1);
-  P.op(OP_MUL, S_L1, S_T2, S_F0);        // l1 = conj(y36 a18 b12) f
+  P.op(OP_MUL, S_L1, S_T1, S_F0, kConjA);  // l1 = conj(y36 a18 b12) f
   P.op(OP_MUL, S_T0, S_Y36, S_A30);
   P.op(OP_MUL, S_T1, S_T0, S_B18);
   P.op(OP_SQR, S_T2, S_F0);
-  P.op(OP_MUL, S_T0, S_T1, S_T2);
-  P.op(OP_CONJ, S_L0, S_T0);             // l0 = conj(y36 a30 b18 f^2)
+  P.op(OP_MUL, S_T0, S_T1, S_T2);        // l0 = conj(T0) = conj(y36 a30 b18 f^2), applied below
   P.op(OP_FROB, S_T1, S_L1, 0, 1);
-  P.op(OP_MUL, S_E0, S_L0, S_T1);
+  P.op(OP_MUL, S_E0, S_T0, S_T1, kConjA);
   P.op(OP_FROB, S_T2, S_L2, 0, 2);
   P.op(OP_MUL, S_E1, S_E0, S_T2);
   P.op(OP_FROB, S_T0, S_F0, 0, 3);
@@ -1377,7 +1380,7 @@ __global__ void __launch_bounds__(wg::kThreads) k_decide_wg(const G1Aff* __restr
     Fq2* dst = S + 6 * op.dst;
     const Fq2* a = opnd(op.a);
     switch (op.code) {
-      case OP_MUL: w_mul(Ln, dst, a, opnd(op.b)); break;
+      case OP_MUL: w_mul(Ln, dst, a, opnd(op.b), op.imm); break;
       case OP_SQR: w_sqr(Ln, dst, a); break;
       case OP_FROB: w_frob(Ln, dst, a, op.imm, gam); break;
       case OP_CONJ: w_conj(dst, a, true); break;

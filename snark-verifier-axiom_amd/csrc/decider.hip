@@ -1089,7 +1089,8 @@ constexpr StepTab make_steps() {
 constexpr int kStepPairs = (make_steps().n - 1) / 2;
 enum WSlot {
   S_F0, S_F1, S_FI, S_AC, S_NN, S_NI, S_TAB, S_X0 = S_TAB + 8, S_X1, S_FX, S_FX2, S_FX3, S_A, S_B, S_C, S_B6, S_B12,
-  S_B18, S_A6, S_A12, S_A18, S_A30, S_Y, S_Y36, S_L0, S_L1, S_L2, S_T0, S_T1, S_T2, S_E0, S_E1, S_E2, S_GT, kSlots
+  S_B18, S_A6, S_A12, S_A18, S_A30, S_Y, S_Y36, S_L0, S_L1, S_L2, S_T0, S_T1, S_T2, S_E0, S_E1, S_E2, S_GT, kSlots,
+  S_F0SQ = S_TAB + 4  // (the power table's upper half, free since round 6: no conjugate entries)
 };
 constexpr int kMaxOps = 512;
 struct WProg {
@@ -1104,11 +1105,26 @@ struct WProg {
   // cyclotomic subgroup), which OP_MUL applies as a sign of its odd-index terms (kConjB) -- round 6:
   // no OP_COPY / OP_CONJ ops (15 per pow_x, ~800 cycles each); the chain ping-pongs between S_X0
   // and S_X1
-  constexpr void pow_x(int dst, int a) {
+  // sq / cube: slots already holding a^2 / a^3 (the hard part forms them just before two of the
+  // three calls), else formed here; sq_out: a slot to keep a^2 in (else S_X0, which the chain reuses)
+  constexpr void pow_x(int dst, int a, int sq = -1, int cube = -1, int sq_out = -1) {
     const XNaf xn = make_xnaf();
-    op(OP_SQR, S_X0, a);
-    for (int e = 1; e < 4; e++) op(OP_MUL, S_TAB + e, e == 1 ? a : S_TAB + e - 1, S_X0);
-    auto entry = [a](int d) { const int e = ((d > 0 ? d : -d) - 1) / 2; return e == 0 ? a : S_TAB + e; };
+    int a2 = sq;
+    if (a2 < 0) {
+      a2 = sq_out >= 0 ? sq_out : S_X0;
+      op(OP_SQR, a2, a);
+    }
+    int a3 = cube;
+    if (a3 < 0) {
+      a3 = S_TAB + 1;
+      op(OP_MUL, a3, a, a2);
+    }
+    op(OP_MUL, S_TAB + 2, a3, a2);
+    op(OP_MUL, S_TAB + 3, S_TAB + 2, a2);
+    auto entry = [a, a3](int d) {
+      const int e = ((d > 0 ? d : -d) - 1) / 2;
+      return e == 0 ? a : (e == 1 ? a3 : S_TAB + e);
+    };
     int r = entry(xn.d[xn.len - 1]);  // (the NAF's top digit is positive)
     for (int i = xn.len - 2; i >= 0; i--) {
       const int d = xn.d[i];
@@ -1155,20 +1171,20 @@ constexpr WProg make_wprog(bool paired = false) {
   // itself (tests only) divides at the end: ops[nv, n).
   P.op(OP_FROB, S_C, S_F1, 0, 2);
   P.op(OP_MUL, S_F0, S_C, S_F1);         // w_0 = f^(p^2 + 1), standing for K_F = conj(w_0) / w_0
-  P.pow_x(S_FX, S_F0);
+  P.pow_x(S_FX, S_F0, -1, -1, S_F0SQ);  // f^2 kept for l0 below
   P.op(OP_SQR, S_A, S_FX);
   P.op(OP_MUL, S_B, S_A, S_FX);
   P.op(OP_SQR, S_B6, S_B);
   P.op(OP_SQR, S_B12, S_B6);
   P.op(OP_MUL, S_B18, S_B12, S_B6);
-  P.pow_x(S_FX2, S_FX);
+  P.pow_x(S_FX2, S_FX, S_A, S_B);        // fx^2, fx^3 from just above
   P.op(OP_SQR, S_A, S_FX2);
   P.op(OP_MUL, S_B, S_A, S_FX2);
   P.op(OP_SQR, S_A6, S_B);
   P.op(OP_SQR, S_A12, S_A6);
   P.op(OP_MUL, S_A18, S_A12, S_A6);
   P.op(OP_MUL, S_A30, S_A18, S_A12);
-  P.pow_x(S_FX3, S_FX2);
+  P.pow_x(S_FX3, S_FX2, S_A, S_B);       // fx2^2, fx2^3 from just above
   P.op(OP_SQR, S_A, S_FX3);
   P.op(OP_SQR, S_B, S_A);
   P.op(OP_SQR, S_Y, S_B);                // fx3^8
@@ -1181,8 +1197,7 @@ constexpr WProg make_wprog(bool paired = false) {
   P.op(OP_MUL, S_L1, S_T1, S_F0, kConjA);  // l1 = conj(y36 a18 b12) f
   P.op(OP_MUL, S_T0, S_Y36, S_A30);
   P.op(OP_MUL, S_T1, S_T0, S_B18);
-  P.op(OP_SQR, S_T2, S_F0);
-  P.op(OP_MUL, S_T0, S_T1, S_T2);        // l0 = conj(T0) = conj(y36 a30 b18 f^2), applied below
+  P.op(OP_MUL, S_T0, S_T1, S_F0SQ);      // l0 = conj(T0) = conj(y36 a30 b18 f^2), applied below
   P.op(OP_FROB, S_T1, S_L1, 0, 1);
   P.op(OP_MUL, S_E0, S_T0, S_T1, kConjA);
   P.op(OP_FROB, S_T2, S_L2, 0, 2);

@@ -45,7 +45,7 @@ rng = np.random.default_rng(1)
 perm = rng.permutation(n)
 rf_shuf = svgpu.make_refs(S.ctypes.data + 32 * perm.astype(np.uint64), B.ctypes.data + 64 * perm.astype(np.uint64))
 for spec in specs:
-    for k in ("SVGPU_H2D_PIECES", "SVGPU_H2D_SPLIT", "SVGPU_GLV", "SVGPU_H2D_STAGE"):
+    for k in ("SVGPU_H2D_PIECES", "SVGPU_H2D_SPLIT", "SVGPU_GLV", "SVGPU_H2D_STAGE", "SVGPU_H2D_RING", "SVGPU_H2D_RING_SLOTS"):
         os.environ.pop(k, None)
     for kv in filter(None, spec.split(" ")):
         k, v = kv.split("=")
@@ -54,7 +54,7 @@ for spec in specs:
     rms, rr = t(lambda: svgpu.msm_refs(rf_shuf, M))
     print(f"host [{spec or 'default'}]  {ms:7.3f} ms  x{ms / dms:.2f}  ok={r == ref}   refs {rms:7.3f} ms  "
           f"x{rms / dms:.2f}  ok={rr == ref}", flush=True)
-for k in ("SVGPU_H2D_PIECES", "SVGPU_H2D_SPLIT", "SVGPU_GLV", "SVGPU_H2D_STAGE"):
+for k in ("SVGPU_H2D_PIECES", "SVGPU_H2D_SPLIT", "SVGPU_GLV", "SVGPU_H2D_STAGE", "SVGPU_H2D_RING", "SVGPU_H2D_RING_SLOTS"):
     os.environ.pop(k, None)
 rng = np.random.default_rng(1)
 perm = rng.permutation(n)

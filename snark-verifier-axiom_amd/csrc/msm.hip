@@ -1637,16 +1637,17 @@ static uint32_t plan_K(uint64_t entries, uint32_t nbt) {
 }
 
 // Host-fed pieces (a fraction of the points over the whole bucket set, so few entries per bucket):
-// chunks of about two average buckets while that stays <= 32 entries (fewer crossing buckets for
-// k_fixup), else max(32, one average bucket); a multiple of 8.  Measured device-resident at the
-// 2^20 plan's window (c = 16, GLV), best accumulate + fixup: 2^16 points K = 8 (average bucket 4),
-// 2^17 16 (8), 3 * 2^16 24 (12), 2^18 32 (16), 349525 24-32 (21; K = 21 and 42: +8-20 %), 2^19
-// 32 (32), 2^20 64 (64) -- tools/gpu_r03_pieceK.sh.
+// chunks of about one average bucket, a multiple of 8, at least 16.  Round 3 (the 32-bit chain,
+// measured device-resident at the 2^20 plan's window) had found about two average buckets best while
+// that stayed <= 32 entries: a segment end then cost ~110 VALU instructions.  With the round-6
+// chain's raw-record segment ends, a quarter-size piece's accumulate at K = 32 filled only half the
+// chip's block slots; one average bucket (K = 24, 16, 16, 16 for the 2^20 pieces 5,4,4,3) measured
+// 2.538-2.570 ms per host-fed 2^20 MSM against 2.602-2.609 (SVGPU_ACC_K = 16 for every piece, two
+// passes, profiles/r06_host_piece_k.log).
 static uint32_t piece_K(uint64_t entries, uint32_t nbt) {
   if (getenv("SVGPU_ACC_K")) return plan_K(entries, nbt);
   const uint64_t avg = entries / nbt;
-  uint64_t K = 2 * avg <= 32 ? 2 * avg : std::max<uint64_t>(32, avg);
-  K = std::min<uint64_t>(std::max<uint64_t>((K + 7) / 8 * 8, 8), 256);
+  const uint64_t K = std::min<uint64_t>(std::max<uint64_t>((avg + 7) / 8 * 8, 16), 256);
   return (uint32_t)K;
 }
 

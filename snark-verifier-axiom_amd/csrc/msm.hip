@@ -224,6 +224,13 @@ __device__ __forceinline__ void for_each_digit(const Fr& s, F&& f) {
   }
 }
 
+__device__ __forceinline__ Fr scalar_in(const uint4 q0, const uint4 q1, int mont_in, uint32_t* __restrict__ err) {
+  Fr s;
+  s.v[0] = q0.x; s.v[1] = q0.y; s.v[2] = q0.z; s.v[3] = q0.w;
+  s.v[4] = q1.x; s.v[5] = q1.y; s.v[6] = q1.z; s.v[7] = q1.w;
+  if (err && !s.is_reduced()) atomicOr(err, 2u);
+  return mont_in ? fe_from_mont(s) : s;
+}
 __device__ __forceinline__ Fr load_scalar(const Fr* __restrict__ scalars, uint32_t i, int mont_in,
                                           uint32_t* __restrict__ err) {
   const uint4* p = reinterpret_cast<const uint4*>(scalars + i);
@@ -249,7 +256,9 @@ struct Digits {
   uint32_t sgn[GLV ? 2 : 1];
   __device__ __forceinline__ void load(const Fr* __restrict__ scalars, uint32_t i, int mont_in,
                                        uint32_t* __restrict__ err) {
-    const Fr s = load_scalar(scalars, i, mont_in, err);
+    from(load_scalar(scalars, i, mont_in, err));
+  }
+  __device__ __forceinline__ void from(const Fr& s) {
     if constexpr (GLV) {
       uint32_t h1[4], h2[4];
       glv_split(s.v, h1, h2);
@@ -379,9 +388,8 @@ __device__ __forceinline__ void ld_rec29(const uint2* __restrict__ o, r29::F& x,
 // uint4 per point of the r29 table (its buffer is carved in uint4): GLV two 72-B records, else one
 // (padded to 80 B per point so host-fed pieces' table slices stay uint4-aligned)
 __host__ __device__ constexpr size_t vtab_uint4_per_point(bool glv) { return glv ? 9 : 5; }
-__device__ __forceinline__ void vtab_put(const G1Aff* __restrict__ bases, uint32_t i, uint4* __restrict__ vtab,
-                                         uint32_t nsplit, bool glv, uint32_t* __restrict__ err) {
-  const G1Aff a = load_aff(bases, i);
+__device__ __forceinline__ void vtab_put_pt(const G1Aff& a, uint32_t i, uint4* __restrict__ vtab, uint32_t nsplit,
+                                            bool glv, uint32_t* __restrict__ err) {
   if (err && (!a.x.is_reduced() || !a.y.is_reduced())) atomicOr(err, 1u);
   const r29::F y = r29::to_r29(a.y.v), x = r29::to_r29(a.x.v);  // below 2p
   uint2* t = reinterpret_cast<uint2*>(vtab);
@@ -394,6 +402,10 @@ __device__ __forceinline__ void vtab_put(const G1Aff* __restrict__ bases, uint32
     for (int j = 0; j < r29::L; j++) beta.v[j] = kBeta29[j];
     st_rec29(t + kVtabRec * ((size_t)nsplit + i), r29::mul(x, beta), y);  // below 2p
   }
+}
+__device__ __forceinline__ void vtab_put(const G1Aff* __restrict__ bases, uint32_t i, uint4* __restrict__ vtab,
+                                         uint32_t nsplit, bool glv, uint32_t* __restrict__ err) {
+  vtab_put_pt(load_aff(bases, i), i, vtab, nsplit, glv, err);
 }
 // Host-fed pieces with the 29-bit chain: the piece's table once its bases have landed
 __global__ void k_vtab(const G1Aff* __restrict__ bases, uint32_t n, uint4* __restrict__ vtab, int glv,
@@ -502,7 +514,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scal
                                                      uint32_t* __restrict__ err, const G1Aff* __restrict__ bases,
                                                      uint4* __restrict__ phix, int phi64, int check_bases,
                                                      int xcd, int bm, uint32_t w0, uint32_t nw,
-                                                     uint4* __restrict__ stored) {
+                                                     uint4* __restrict__ stored, int pf) {
   using D = Digits<C, GLV>;
   constexpr int W = D::W, LOGB = C - 1;
   constexpr int CB = coarse_bits(C, D::NB), FB = LOGB - CB, NBIN = 1 << CB;
@@ -515,6 +527,41 @@ __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scal
   constexpr uint32_t CH = sort_chunk(D::EP);
   const uint32_t blk = sort_block(blockIdx.x, gridDim.x, xcd);
   const uint32_t lo = blk * CH, hi = min(n, lo + CH);
+  auto count = [&](const D& d) {
+    d.each([&](int w, uint32_t mag, uint32_t, uint32_t) {
+      if (mag && (uint32_t)w - w0 < nw) atomicAdd(&h[(w - w0) * NBIN + ((mag - 1) >> FB)], 1u);
+    });
+  };
+  if (phix && phi64 == kPhiVtab && pf) {
+    // Round 6: the 29-bit table path with the next point's scalar and base loaded one iteration
+    // ahead (the pass is load-latency-bound: ~4 dependent iterations per thread at 4 waves/SIMD)
+    uint32_t i = lo + threadIdx.x;
+    const uint4* sp = reinterpret_cast<const uint4*>(scalars);
+    const uint4* bp = reinterpret_cast<const uint4*>(bases);
+    uint4 s0{}, s1{}, b0{}, b1{}, b2{}, b3{};
+    if (i < hi) {
+      s0 = sp[2 * (size_t)i], s1 = sp[2 * (size_t)i + 1];
+      b0 = bp[4 * (size_t)i], b1 = bp[4 * (size_t)i + 1], b2 = bp[4 * (size_t)i + 2], b3 = bp[4 * (size_t)i + 3];
+    }
+    for (; i < hi; i += kBlock) {
+      G1Aff a;
+      a.x.v[0] = b0.x; a.x.v[1] = b0.y; a.x.v[2] = b0.z; a.x.v[3] = b0.w;
+      a.x.v[4] = b1.x; a.x.v[5] = b1.y; a.x.v[6] = b1.z; a.x.v[7] = b1.w;
+      a.y.v[0] = b2.x; a.y.v[1] = b2.y; a.y.v[2] = b2.z; a.y.v[3] = b2.w;
+      a.y.v[4] = b3.x; a.y.v[5] = b3.y; a.y.v[6] = b3.z; a.y.v[7] = b3.w;
+      const uint4 c0 = s0, c1 = s1;
+      const uint32_t j = i + kBlock;
+      if (j < hi) {
+        s0 = sp[2 * (size_t)j], s1 = sp[2 * (size_t)j + 1];
+        b0 = bp[4 * (size_t)j], b1 = bp[4 * (size_t)j + 1], b2 = bp[4 * (size_t)j + 2], b3 = bp[4 * (size_t)j + 3];
+      }
+      vtab_put_pt(a, i, phix, n, GLV, check_bases ? err : nullptr);
+      D d;
+      d.from(scalar_in(c0, c1, mont_in, err));
+      if (stored) d.store(stored, i);
+      count(d);
+    }
+  } else
   for (uint32_t i = lo + threadIdx.x; i < hi; i += kBlock) {
     // Montgomery bases are checked here (canonical ones by k_to_mont_bases)
     if (phix && phi64 == kPhiVtab) {  // the 29-bit chain's table (n = nsplit on the device path)
@@ -530,9 +577,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_hist(const Fr* __restrict__ scal
     D d;
     d.load(scalars, i, mont_in, err);
     if (stored) d.store(stored, i);
-    d.each([&](int w, uint32_t mag, uint32_t, uint32_t) {
-      if (mag && (uint32_t)w - w0 < nw) atomicAdd(&h[(w - w0) * NBIN + ((mag - 1) >> FB)], 1u);
-    });
+    count(d);
   }
   __syncthreads();
   // bm: block-major bcnt[blk * nk + key], one contiguous row per block (the scan reads it in
@@ -1810,8 +1855,10 @@ static int msm_sort(const MsmPlan& p, const MsmScratch& w, const SortOut& so, co
   static const int xcd = !getenv("SVGPU_SORT_XCD") || atoi(getenv("SVGPU_SORT_XCD")) != 0 ? 1 : 0;
   // block-major per-block counts + the tiled scan (SVGPU_SORT_BM=0: key-major, k_bin_scan_chunks)
   static const int bm = !getenv("SVGPU_SORT_BM") || atoi(getenv("SVGPU_SORT_BM")) != 0 ? 1 : 0;
+  // SVGPU_HIST_PF=0 (read per call): the histogram pass without the one-ahead loads (29-bit table path)
+  const int hist_pf = !getenv("SVGPU_HIST_PF") || atoi(getenv("SVGPU_HIST_PF")) != 0;
   SV_LAUNCH_C(k_bin_hist, p.glv, p.c, dim3(nblk), dim3(kBlock), scalars, npts, mont_in, nblk, w.bcnt, w.err, bases,
-              phix, p.r29 ? kPhiVtab : p.phi64, check_bases, xcd, bm, w0, nw, stored);
+              phix, p.r29 ? kPhiVtab : p.phi64, check_bases, xcd, bm, w0, nw, stored, hist_pf);
   SV_HIP(hipGetLastError());
   if (ev_sort_mid) SV_HIP(hipEventRecord(ev_sort_mid, st));
   if (bm) {

@@ -101,6 +101,38 @@ def test_sort_stored_halves(gpu, oracle_cpp, monkeypatch, halves, glv, bits):
                   svgpu.SV_MONTGOMERY) == exp
 
 
+@pytest.mark.parametrize("pf", ["0", "1"])
+def test_hist_prefetch(gpu, oracle_cpp, monkeypatch, pf):
+    """The histogram pass with the next point's loads one iteration ahead (round 6, the 29-bit table
+    path) against the plain loop: a ragged size (the last block partial, threads whose next point
+    is past the end), both input forms, and invalid Montgomery inputs still flagged (a scalar not
+    below r, a base coordinate not below p) from inside the prefetching loop."""
+    from svgpu import device as dv
+    from svgpu import encoding as enc
+    import svgpu
+    monkeypatch.setenv("SVGPU_HIST_PF", pf)
+    n = 40001
+    B = oracle_cpp.gen_bases(b.SEED_BASES, n, start=7 * n)
+    S = oracle_cpp.gen_scalars(b.SEED_SCALARS, n, start=7 * n)
+    exp = _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
+    assert dv.msm(torch.from_numpy(B.view(np.int64)).to(gpu), torch.from_numpy(S.view(np.int64)).to(gpu),
+                  svgpu.SV_CANONICAL) == exp
+    Sm = enc.scalars_array([enc.limbs_to_int(r) for r in S], svgpu.SV_MONTGOMERY)
+    Bm = enc.bases_array([enc.g1_from_limbs(r) for r in B], svgpu.SV_MONTGOMERY)
+    assert dv.msm(torch.from_numpy(Bm.view(np.int64)).to(gpu), torch.from_numpy(Sm.view(np.int64)).to(gpu),
+                  svgpu.SV_MONTGOMERY) == exp
+    bad_s = Sm.copy()
+    bad_s[n - 1] = enc.ints_to_limbs([b.R])[0]  # the last point: reached through the prefetch
+    with pytest.raises(svgpu.ArgumentError):
+        dv.msm(torch.from_numpy(Bm.view(np.int64)).to(gpu), torch.from_numpy(bad_s.view(np.int64)).to(gpu),
+               svgpu.SV_MONTGOMERY)
+    bad_b = Bm.copy()
+    bad_b[n - 1][:4] = enc.ints_to_limbs([b.P])[0]  # x = p: not reduced
+    with pytest.raises(svgpu.ArgumentError):
+        dv.msm(torch.from_numpy(bad_b.view(np.int64)).to(gpu), torch.from_numpy(Sm.view(np.int64)).to(gpu),
+               svgpu.SV_MONTGOMERY)
+
+
 def test_adversarial_single_bucket(gpu, oracle_cpp):
     """All scalars equal: every window's digits land in ONE bucket (maximal bucket skew)."""
     import svgpu

@@ -14,7 +14,7 @@ log_n = arg
 B = dv.gen_bases(dv.empty_bases(n, dev), ob.SEED_BASES, 0)
 S = dv.gen_scalars(dv.empty_scalars(n, dev), ob.SEED_SCALARS, 0)
 torch.cuda.synchronize()
-KEYS = ("SVGPU_HIST_PF", "SVGPU_ACC_LOOP", "SVGPU_GLV", "SVGPU_MSM_LEAN", "SVGPU_ACC_K", "SVGPU_RED_LOG", "SVGPU_WINDOW_BITS", "SVGPU_GLV_MAX_LOG", "SVGPU_SORT_E32", "SVGPU_GROUP_P", "SVGPU_GLV_PHI64", "SVGPU_SORT_FORK", "SVGPU_SORT_HALVES")
+KEYS = ("SVGPU_HIST_PF", "SVGPU_GLV", "SVGPU_MSM_LEAN", "SVGPU_ACC_K", "SVGPU_RED_LOG", "SVGPU_WINDOW_BITS", "SVGPU_GLV_MAX_LOG", "SVGPU_SORT_E32", "SVGPU_GROUP_P", "SVGPU_GLV_PHI64", "SVGPU_SORT_FORK", "SVGPU_SORT_HALVES")
 BASE = {k: os.environ[k] for k in KEYS if k in os.environ}
 ref = None
 for rnd in range(int(os.environ.get("SWEEP_ROUNDS", "2"))):

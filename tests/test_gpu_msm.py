@@ -335,8 +335,9 @@ def test_bucket_reduction_paths(gpu, oracle_cpp, monkeypatch, path, glv):
 
 @pytest.mark.parametrize("chain", ["1", "0"])
 def test_accumulate_chains(gpu, oracle_cpp, monkeypatch, chain):
-    """k_accumulate's two chains (SVGPU_ACC_R29: 9 x 29-bit limbs with the sums stored as x R' words
-    and converted by k_fixup / bucket_at, or 8 x 32-bit limbs), with every reader of the stored sums:
+    """k_accumulate's two chains (SVGPU_ACC_R29: 9 x 29-bit limbs with the sums stored as the chain's
+    own limb records and converted once per bucket by their readers, or 8 x 32-bit limbs), with every
+    reader of the stored sums:
     the default tree, the plain k_wsum reduction, host-fed pieces (ADD mode: owner segments start
     from the stored sums), repeated points (the doubling folded into the addition), P + (-P), and
     one skewed bucket (k_fixup's heavy queue), against the reference Pippenger (msm.rs:238-316)."""
@@ -362,6 +363,36 @@ def test_accumulate_chains(gpu, oracle_cpp, monkeypatch, chain):
     S2 = oracle_cpp.gen_scalars(b.SEED_SCALARS, n2, start=3)
     S2[: n2 // 2] = S2[0]  # half the points in one bucket per window
     assert svgpu.msm_arrays(B2, S2, svgpu.SV_CANONICAL) == _to_pt(oracle_cpp.msm_pippenger(B2, S2, 0))
+
+
+@pytest.mark.parametrize("fed", ["device", "host_pieces"])
+def test_chain_cancels_and_restarts(gpu, oracle_cpp, monkeypatch, fed):
+    """Round 6's chain state is never the identity: a P + (-P) inside a chunk empties it and the next
+    point restarts it; a chunk that ends empty stores the identity record (ZZ = 0) that k_fixup, the
+    in-block join, the tree and the host-fed pieces' ADD mode must read as such.  All scalars equal
+    (every window's entries in ONE bucket), points (A_0, -A_0, A_1, -A_1, ...) plus one extra Z: every
+    pair cancels, at every chunk position, and the MSM is s Z; then the pairs reversed (-A_i, A_i)
+    and a doubling pair (Z, Z) in the middle.  Against the reference Pippenger (msm.rs:238-316)."""
+    import svgpu
+    from svgpu import encoding as enc
+    n_pairs = (1 << 15) // 2 if fed == "host_pieces" else 2048
+    if fed == "host_pieces":
+        monkeypatch.setenv("SVGPU_H2D_PIECES", "3")
+    A = oracle_cpp.gen_bases(b.SEED_BASES, n_pairs + 1, start=91)
+    pts = [enc.g1_from_limbs(r) for r in A]
+    z = pts[-1]
+    for flip in (False, True):
+        seq = []
+        for p in pts[:-1]:
+            q = b.g1_neg(p)
+            seq += [q, p] if flip else [p, q]
+        if flip:
+            seq[n_pairs: n_pairs] = [z, z]   # a doubling in the middle of the bucket
+        seq.append(z)
+        B = enc.bases_array(seq)
+        S = np.repeat(enc.scalars_array([0x1234567890ABCDEF1234567890ABCDEF]), len(seq), axis=0)
+        exp = _to_pt(oracle_cpp.msm_pippenger(B, S, 0))
+        assert svgpu.msm_arrays(B, S, svgpu.SV_CANONICAL) == exp, (fed, flip)
 
 
 @pytest.mark.parametrize("chain", ["1", "0"])

@@ -41,9 +41,11 @@ MAC_PEAK = 64 * 256 * 2.4e9
 MAC_PEAK_MEASURED = 64 * 4 / 4.25 * 256 * 2.4e9
 MACS_PER_FPMUL = 136             # 8-limb CIOS: 64 + 64 + 8
 # v_mad_u64_u32 per bucket entry that k_accumulate<false, true, 1> (the 29-bit chain) issues on its
-# common path (no segment end, no doubling): tools/isa_count.py over the compiler's assembly
-# (81 + 81 per product, 45 + 81 per square, 243 for the fused Y3 pair, + 36)
-MADS_PER_ENTRY_R29 = 1503
+# common path (no segment end, no doubling, no cancellation): r29::madd_live's nine field products --
+# mul_sub<8> and five mul at 81 + 81, the square and sqr_sub2c<6> at 45 + 81, the fused Y3 pair
+# mul_sum2 at 243 -- = 1467 (round 6; rounds 4-5's madd issued 1503).  The compiled loop's common
+# blocks hold 1482 (tools/isa_count.py), the other 15 being address arithmetic.
+MADS_PER_ENTRY_R29 = 1467
 BYTES_PER_POINT = 96             # 64 B affine base + 32 B scalar, read once
 # Decider algorithmic work: Fq products of ONE decide, COUNTED by instrumenting the C++
 # restatements (oracle/cpu/bn254_ref.cpp; both pinned by tests/test_oracle_cpp.py):

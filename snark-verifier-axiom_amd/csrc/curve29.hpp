@@ -79,30 +79,32 @@ SV29_HD F neg_one() {  // p - R' mod p
   return r;
 }
 SV29_HD Xyzz start(const F& x2, const F& y2, bool neg) { return {x2, y2, one(), neg ? neg_one() : one()}; }
-SV29_HD Xyzz madd_live(const Xyzz& p, const F& x2, const F& y2, bool neg, bool& cancel) {
-  F Pd = mul_sub<8>(x2, p.ZZ, p.X);                  // U2 - X + 8p, fused: < 10p (state X < 8p)
-  F Rd = sub_sgn<4>(mul(y2, p.ZZZ), neg, p.Y);       // +-S2 - Y + 4p: < 6p
-  F X = p.X, Y = p.Y, ZZ = p.ZZ, ZZZ = p.ZZZ;
-  bool dbl = false;
-  if (is_zero_mod_p_10p(Pd)) {
-    if (!is_zero_mod_p_6p(Rd)) {
-      // P + (-P): the caller restarts the chain.  The products below run on as garbage except
-      // ZZ3 = 0 * PP = 0 exactly, so the state reads as the identity (ZZ == 0) if it is stored
-      cancel = true;
-      ZZ = zero();
-    } else {
-      const F x2s = sqr(x2), ys = neg ? sub<2>(zero(), y2) : y2;
-      Pd = add(ys, ys);               // < 4p
-      Rd = add(add(x2s, x2s), x2s);   // < 6p
-      X = x2, Y = ys, ZZ = one(), ZZZ = one();
-      dbl = true;
-    }
-  }
-  const F PP = sqr(Pd), PPP = mul(Pd, PP), Q = mul(X, PP);  // < 2p
-  // X3 = Rd^2 [- PPP] - 2Q + 6p in the square's high columns: in (0, 8p)
-  const F X3 = sqr_sub2c<6>(Rd, dbl ? zero() : PPP, Q);
-  const F Y3 = mul_sum2(Rd, sub<8>(Q, X3), Y, sub<2>(zero(), PPP));
-  return {X3, Y3, mul(ZZ, PP), mul(ZZZ, PPP)};
+// special (round 6, cont.): 0 the common case; 1 P + (-P), whose result is meaningless except that
+// the caller marks the chain empty and zeroes ZZ (a stored empty chain reads as the identity); 2 the
+// doubling P + P, whose result the caller replaces by dbl_start.  Both rare cases leave madd_live's
+// products running on as garbage.
+SV29_HD Xyzz madd_live(const Xyzz& p, const F& x2, const F& y2, bool neg, int& special) {
+  const F Pd = mul_sub<8>(x2, p.ZZ, p.X);                  // U2 - X + 8p, fused: < 10p (state X < 8p)
+  const F Rd = sub_sgn<4>(mul(y2, p.ZZZ), neg, p.Y);       // +-S2 - Y + 4p: < 6p
+  if (is_zero_mod_p_10p(Pd)) special = is_zero_mod_p_6p(Rd) ? 2 : 1;
+  const F PP = sqr(Pd), PPP = mul(Pd, PP), Q = mul(p.X, PP);  // < 2p
+  // X3 = Rd^2 - PPP - 2Q + 6p in the square's high columns: in (0, 8p)
+  const F X3 = sqr_sub2c<6>(Rd, PPP, Q);
+  const F Y3 = mul_sum2(Rd, sub<8>(Q, X3), p.Y, sub<2>(zero(), PPP));
+  return {X3, Y3, mul(p.ZZ, PP), mul(p.ZZZ, PPP)};
+}
+// 2 (x2, +-y2) as a chain state (madd_live's special == 2): dbl-2008-s-1 at Z = 1 -- the same
+// products as the addition with Pd = 2y, Rd = 3x^2, U1 = x, S1 = y and no PPP term in X3; ZZ3 = PP,
+// ZZZ3 = PPP (ZZ = ZZZ = 1).  Bounds as madd_live's: X3 < 8p, the rest < 2p.
+SV29_HD Xyzz dbl_start(const F& x2, const F& y2, bool neg) {
+  const F ys = neg ? sub<2>(zero(), y2) : y2;  // < 2p (y2 < 2p)
+  const F x2s = sqr(x2);
+  const F Pd = add(ys, ys);               // < 4p
+  const F Rd = add(add(x2s, x2s), x2s);   // < 6p
+  const F PP = sqr(Pd), PPP = mul(Pd, PP), Q = mul(x2, PP);
+  const F X3 = sqr_sub2c<6>(Rd, zero(), Q);
+  const F Y3 = mul_sum2(Rd, sub<8>(Q, X3), ys, sub<2>(zero(), PPP));
+  return {X3, Y3, PP, PPP};
 }
 
 // p + q, both XYZZ states (bounds as above; either may be the identity).  add-2008-s; the

@@ -1083,9 +1083,16 @@ __global__ void __launch_bounds__(kBlock, R29 ? SV_ACC29_MIN_BLOCKS : SV_ACC_MIN
           }
         }
         if (live && !fresh) {
-          bool cancel = false;
-          acc = r29::madd_live(acc, x, y, neg, cancel);
-          if (cancel) empty = true;
+          int special = 0;
+          acc = r29::madd_live(acc, x, y, neg, special);
+          if (special) {  // rare, divergent: P + P, or P + (-P) (the chain restarts at its next point)
+            if (special == 2) {
+              acc = r29::dbl_start(x, y, neg);
+            } else {
+              acc.ZZ = r29::zero();  // a chain that ends empty stores the identity
+              empty = true;
+            }
+          }
         }
       }
     } else

@@ -56,8 +56,9 @@ static F parse(const std::string& h) {
 }
 // "madd" / "maddn" mode: stdin lines "X Y ZZ ZZZ x2 y2" (hex) -> "X3 Y3 ZZ3 ZZZ3" of
 // state + (x2, y2) / state + (x2, -y2).  "maddl" / "maddln": the round-6 loop's pair -- an
-// identity state takes start(x2, +-y2), any other madd_live; a cancelled state must have ZZ == 0 (the
-// loop marks its chain empty and a stored one reads as the identity), X and Y are left as they are.
+// identity state takes start(x2, +-y2), any other madd_live (its doubling case replaced by dbl_start,
+// its cancellation zeroing ZZ, as the loop does: the loop marks that chain empty and a stored one
+// reads as the identity by ZZ == 0).
 static bool g_neg = false, g_live = false;
 static int madd_mode() {
   char buf[6][80];
@@ -69,9 +70,11 @@ static int madd_mode() {
     } else if (is_identity(st)) {
       r = start(parse(buf[4]), parse(buf[5]), g_neg);
     } else {
-      bool cancel = false;
-      r = madd_live(st, parse(buf[4]), parse(buf[5]), g_neg, cancel);
-      if (cancel && !is_identity(r)) r.ZZ.v[0] = 1;  // the loop reads a cancelled state by ZZ == 0
+      // as the loop runs it: the doubling replaced by dbl_start, a cancellation zeroes ZZ
+      int special = 0;
+      r = madd_live(st, parse(buf[4]), parse(buf[5]), g_neg, special);
+      if (special == 2) r = dbl_start(parse(buf[4]), parse(buf[5]), g_neg);
+      else if (special == 1) r.ZZ = zero();
     }
     pr(r.X), pr(r.Y), pr(r.ZZ), pr(r.ZZZ);
     printf("\n");

@@ -4,12 +4,12 @@ python tools/isa_count.py [KERNEL_SUBSTRING [SOURCE]]   (default: the 29-bit buc
 k_accumulate<false, true, 1> of csrc/msm.hip; e.g. `k_decide_wg decider.hip` for the decider)
 
 Compiles snark-verifier-axiom_amd/csrc/msm.hip with hipcc -S (device only), takes the kernel's body,
-and splits it at its basic blocks.  The XYZZ mixed addition's common path (no segment end, no
-doubling, accumulator not the identity) is the blocks that every iteration executes; the script
-prints the opcode histogram of the whole loop and of the blocks on that path (identified as the
-blocks holding v_mad_u64_u32 outside the rare doubling branch, whose square of x2 is the only
-126-mad block), so that mads per bucket entry come from the code the GPU runs, not from a count of
-the source.
+and prints every basic block's instruction, v_mad_u64_u32 and VALU counts with its branch targets.
+Which blocks form the per-entry common path has to be read off that control flow (the loop's
+back edge, the rare branches it skips): for the round-6 29-bit chain the loop's common blocks hold
+1,482 mads (madd_live's nine products, 1,467, plus address arithmetic), the doubling branch
+(dbl_start) ~950 and the post-loop owner join (r29::add) ~2,280.  Rounds 4-5 identified the path
+by a fixed rule (the doubling branch's lone 126-mad square), which no longer holds.
 """
 import collections
 import os
@@ -63,8 +63,9 @@ def main():
         if n == 0:
             continue
         valu = sum(v for k, v in c.items() if k.startswith("v_"))
-        print("%-10s %6d %6d %6d  %s" % (nm, n, c["v_mad_u64_u32"], valu,
-                                        ", ".join("%s %d" % kv for kv in c.most_common(4))))
+        br = [l.split()[-1] for l in b if "branch" in l]
+        print("%-10s %6d %6d %6d  %s  -> %s" % (nm, n, c["v_mad_u64_u32"], valu,
+                                              ", ".join("%s %d" % kv for kv in c.most_common(4)), " ".join(br)))
     del back
 
 
